@@ -1,0 +1,80 @@
+"""ctypes binding of libfsmi.so (the C ABI declared in include/fsmi.h).
+
+There is deliberately no fallback: if the library is missing or fails to load,
+every hot-path op raises.  Build it with ``python -m foundationstereo_amd.build``
+(or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from .build import LIB
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> argtypes, mirroring include/fsmi.h
+SIGNATURES = {
+    "fsmi_version": [],
+    "fsmi_last_error": [],
+    "fsmi_arch": [],
+    "fsmi_gwc_volume": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_concat_volume": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_comb_volume_stem": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_pointwise_proj": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_allpairs_corr": [_P, _P, _PP, _I, _I, _I, _I, _I, _P],
+    "fsmi_volume_pyramid": [_P, _PP, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_geo_lookup": [_PP, _PP, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_bilinear_sampler_1d": [_P, _P, _P, _I, _I, _I, _I, _P],
+    "fsmi_disparity_regression": [_P, _P, _I, _I, _I, _I, _P],
+    "fsmi_softmax_regression": [_P, _P, _I, _I, _I, _I, _P],
+    "fsmi_context_upsample": [_P, _P, _P, _I, _I, _I, _P],
+    "fsmi_softmax_context_upsample": [_P, _P, _P, _F, _I, _I, _I, _P],
+    "fsmi_gru_reset": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_gru_blend": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "fsmi_timer_enable": [_I],
+    "fsmi_timer_reset": [],
+    "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
+}
+
+KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
+           "gru_reset", "gru_blend"]
+
+_lib = None
+
+
+class FsmiError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libfsmi.so once; raise if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        raise FsmiError(f"libfsmi.so not found at {LIB}: the HIP hot path is not built "
+                        "(run `python -m foundationstereo_amd.build`)")
+    lib = ctypes.CDLL(LIB)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_char_p if name in ("fsmi_last_error", "fsmi_arch") else ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().fsmi_last_error().decode(errors="replace")
+        if rc == 1001:
+            raise FsmiError(f"{what}: {msg}")
+        raise FsmiError(f"{what}: HIP error {rc}: {msg}")
+
+
+def ptr_array(ptrs):
+    arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    return ctypes.cast(arr, _PP), arr

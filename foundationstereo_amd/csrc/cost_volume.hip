@@ -1,0 +1,289 @@
+// Cost-volume construction: group-wise correlation,
+// concat volume, and the fused comb-volume + corr_stem[0] build.
+//
+// Layout: features (B,C,H,W) fp32; volumes (B,Ch,D,H,W) fp32 -- the native
+// NCDHW layout MIOpen's conv3d consumes, so nothing downstream re-packs.
+//
+// Roofline: HBM-bound (arithmetic intensity ~1 flop/B).  One block owns one
+// (b,h) row and a chunk of DC disparities; the row's feature group is staged
+// in LDS once and normalised there, every output lane writes consecutive w so
+// stores are coalesced 256 B per wave-instruction.  Blocks of the same row
+// are placed on one XCD (xcd_remap) so re-staging a row hits that XCD's L2.
+#include "fsmi_common.h"
+
+namespace fsmi {
+namespace {
+
+constexpr int kThreads = 256;
+
+// Stage rows [g*Cg, (g+1)*Cg) of feature map `f` at (b,h) into lds[Cg][W],
+// then L2-normalise every column over the Cg channels (F.normalize, eps 1e-12,
+// core/submodule.py:395).
+__device__ __forceinline__ void stage_group(const float* __restrict__ f, float* lds, int b, int h,
+                                            int g, int Cg, int C, int H, int W) {
+  const size_t plane = static_cast<size_t>(H) * W;
+  const float* src = f + (static_cast<size_t>(b) * C + static_cast<size_t>(g) * Cg) * plane +
+                     static_cast<size_t>(h) * W;
+  if ((W & 3) == 0) {
+    const int W4 = W >> 2;
+    for (int i = threadIdx.x; i < Cg * W4; i += kThreads) {
+      const int c = i / W4, q = i - c * W4;
+      const float4 v = *reinterpret_cast<const float4*>(src + c * plane + 4 * q);
+      *reinterpret_cast<float4*>(lds + c * W + 4 * q) = v;
+    }
+  } else {
+    for (int i = threadIdx.x; i < Cg * W; i += kThreads) {
+      const int c = i / W, w = i - c * W;
+      lds[c * W + w] = src[c * plane + w];
+    }
+  }
+  __syncthreads();
+  for (int w = threadIdx.x; w < W; w += kThreads) {
+    float s = 0.f;
+    for (int c = 0; c < Cg; ++c) {
+      const float v = lds[c * W + w];
+      s += v * v;
+    }
+    const float n = fmaxf(sqrtf(s), 1e-12f);
+    for (int c = 0; c < Cg; ++c) lds[c * W + w] = lds[c * W + w] / n;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float group_dot(const float* L, const float* R, int Cg, int W, int w, int d) {
+  float v = 0.f;
+  for (int c = 0; c < Cg; ++c) v += L[c * W + w] * R[c * W + (w - d)];
+  return v;
+}
+
+// a1: out (B,G,D,H,W)
+template <int NOUT>
+__global__ __launch_bounds__(kThreads) void gwc_kernel(const float* __restrict__ fl, const float* __restrict__ fr,
+                                                       float* __restrict__ out, int C, int G, int D, int H,
+                                                       int W, int DC, int nDC) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Cg = C / G;
+  float* L = smem;
+  float* R = smem + Cg * W;
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = item / nDC, dc = item - row * nDC;
+  const int b = row / H, h = row - b * H;
+  const int d0 = dc * DC, dn = min(DC, D - d0);
+  const size_t plane = static_cast<size_t>(H) * W;
+  for (int g = 0; g < G; ++g) {
+    stage_group(fl, L, b, h, g, Cg, C, H, W);
+    stage_group(fr, R, b, h, g, Cg, C, H, W);
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) {
+      const int j = threadIdx.x + k * kThreads;
+      if (j < dn * W) {
+        const int dl = j / W, w = j - dl * W, d = d0 + dl;
+        const float v = (w >= d) ? group_dot(L, R, Cg, W, w, d) : 0.f;
+        out[((static_cast<size_t>(b) * G + g) * D + d) * plane + static_cast<size_t>(h) * W + w] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// a1 + a2 + corr_stem[0] (1x1x1 conv 32 -> Cs):
+// out[b,o,d,h,w] = A[o,w] + [w>=d] Bm[o,w-d] + sum_g Wg[o,g] gwc_g(d,w)
+template <int G, int NOUT>
+__global__ __launch_bounds__(kThreads) void comb_stem_kernel(const float* __restrict__ fl,
+                                                             const float* __restrict__ fr,
+                                                             const float* __restrict__ A,
+                                                             const float* __restrict__ Bm,
+                                                             const float* __restrict__ Wg,
+                                                             float* __restrict__ out, int C, int Cs, int D,
+                                                             int H, int W, int DC, int nDC) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Cg = C / G;
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = item / nDC, dc = item - row * nDC;
+  const int b = row / H, h = row - b * H;
+  const int d0 = dc * DC, dn = min(DC, D - d0);
+  const size_t plane = static_cast<size_t>(H) * W;
+
+  float acc[NOUT][G];
+#pragma unroll
+  for (int k = 0; k < NOUT; ++k)
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[k][g] = 0.f;
+
+  float* L = smem;
+  float* R = smem + Cg * W;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    stage_group(fl, L, b, h, g, Cg, C, H, W);
+    stage_group(fr, R, b, h, g, Cg, C, H, W);
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) {
+      const int j = threadIdx.x + k * kThreads;
+      if (j < dn * W) {
+        const int dl = j / W, w = j - dl * W, d = d0 + dl;
+        if (w >= d) acc[k][g] = group_dot(L, R, Cg, W, w, d);
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: stage A/Bm rows and the gwc columns of the stem weight
+  float* As = smem;
+  float* Bs = smem + Cs * W;
+  float* Ws = smem + 2 * Cs * W;
+  const float* Ab = A + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
+  const float* Bb = Bm + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
+  for (int i = threadIdx.x; i < Cs * W; i += kThreads) {
+    const int o = i / W, w = i - o * W;
+    As[i] = Ab[o * plane + w];
+    Bs[i] = Bb[o * plane + w];
+  }
+  for (int i = threadIdx.x; i < Cs * G; i += kThreads) Ws[i] = Wg[i];
+  __syncthreads();
+
+#pragma unroll
+  for (int k = 0; k < NOUT; ++k) {
+    const int j = threadIdx.x + k * kThreads;
+    if (j < dn * W) {
+      const int dl = j / W, w = j - dl * W, d = d0 + dl;
+      const bool valid = w >= d;
+      float* dst = out + (static_cast<size_t>(b) * Cs * D + d) * plane + static_cast<size_t>(h) * W + w;
+      for (int o = 0; o < Cs; ++o) {
+        float v = As[o * W + w];
+        if (valid) v += Bs[o * W + w - d];
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < G; ++g) s += Ws[o * G + g] * acc[k][g];
+        dst[static_cast<size_t>(o) * D * plane] = v + s;
+      }
+    }
+  }
+}
+
+// a2: out (B,2C,D,H,W); one thread per output element, w fastest.
+__global__ __launch_bounds__(kThreads) void concat_kernel(const float* __restrict__ pl, const float* __restrict__ pr,
+                                                          float* __restrict__ out, int C, int D, int H, int W,
+                                                          long long total) {
+  const size_t plane = static_cast<size_t>(H) * W;
+  for (long long i = blockIdx.x * static_cast<long long>(kThreads) + threadIdx.x; i < total;
+       i += static_cast<long long>(gridDim.x) * kThreads) {
+    const int w = static_cast<int>(i % W);
+    long long r = i / W;
+    const int h = static_cast<int>(r % H);
+    r /= H;
+    const int d = static_cast<int>(r % D);
+    r /= D;
+    const int c2 = static_cast<int>(r % (2 * C));
+    const int b = static_cast<int>(r / (2 * C));
+    float v;
+    if (c2 < C) {
+      v = pl[(static_cast<size_t>(b) * C + c2) * plane + static_cast<size_t>(h) * W + w];
+    } else {
+      v = (w >= d) ? pr[(static_cast<size_t>(b) * C + (c2 - C)) * plane + static_cast<size_t>(h) * W + (w - d)] : 0.f;
+    }
+    out[i] = v;
+  }
+}
+
+// out[b,o,p] = bias[o] + sum_c Wt[o,c] x[b,c,p]; 8 outputs per thread.
+constexpr int kProjO = 8;
+__global__ __launch_bounds__(kThreads) void proj_kernel(const float* __restrict__ x, const float* __restrict__ Wt,
+                                                        const float* __restrict__ bias, float* __restrict__ out,
+                                                        int C, int O, int P) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];  // [kProjO][C]
+  const int o0 = blockIdx.y * kProjO;
+  const int on = min(kProjO, O - o0);
+  const int b = blockIdx.z;
+  for (int i = threadIdx.x; i < on * C; i += kThreads) wsm[i] = Wt[static_cast<size_t>(o0) * C + i];
+  __syncthreads();
+  const int p = blockIdx.x * kThreads + threadIdx.x;
+  if (p >= P) return;
+  float acc[kProjO];
+#pragma unroll
+  for (int o = 0; o < kProjO; ++o) acc[o] = 0.f;
+  const float* xb = x + static_cast<size_t>(b) * C * P + p;
+  for (int c = 0; c < C; ++c) {
+    const float v = xb[static_cast<size_t>(c) * P];
+#pragma unroll
+    for (int o = 0; o < kProjO; ++o)
+      if (o < on) acc[o] += wsm[o * C + c] * v;
+  }
+#pragma unroll
+  for (int o = 0; o < kProjO; ++o)
+    if (o < on) out[(static_cast<size_t>(b) * O + o0 + o) * P + p] = acc[o] + (bias ? bias[o0 + o] : 0.f);
+}
+
+constexpr int kNout = 8;
+
+inline int pick_dc(int D, int W) { return max(1, min(D, kNout * kThreads / W)); }
+
+}  // namespace
+}  // namespace fsmi
+
+using namespace fsmi;
+
+extern "C" {
+
+int fsmi_gwc_volume(const float* fl, const float* fr, float* out, int B, int C, int G, int D, int H, int W,
+                    void* stream) {
+  FSMI_CHECK_ARG(fl && fr && out, "fsmi_gwc_volume: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && G > 0 && D > 0 && H > 0 && W > 0, "fsmi_gwc_volume: bad shape");
+  FSMI_CHECK_ARG(C % G == 0, "C:%d, num_groups:%d", C, G);
+  const int Cg = C / G;
+  const size_t lds = static_cast<size_t>(2) * Cg * W * sizeof(float);
+  FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_gwc_volume: row too large for LDS (Cg=%d W=%d)", Cg, W);
+  const int DC = pick_dc(D, W);
+  const int nDC = (D + DC - 1) / DC;
+  const unsigned grid = static_cast<unsigned>(B) * H * nDC;
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_GWC, s);
+  hipLaunchKernelGGL(gwc_kernel<kNout>, dim3(grid), dim3(kThreads), lds, s, fl, fr, out, C, G, D, H, W, DC, nDC);
+  return finish_launch("fsmi_gwc_volume");
+}
+
+int fsmi_concat_volume(const float* pl, const float* pr, float* out, int B, int C, int D, int H, int W,
+                       void* stream) {
+  FSMI_CHECK_ARG(pl && pr && out, "fsmi_concat_volume: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && D > 0 && H > 0 && W > 0, "fsmi_concat_volume: bad shape");
+  const long long total = static_cast<long long>(B) * 2 * C * D * H * W;
+  const unsigned grid = static_cast<unsigned>(std::min<long long>((total + kThreads - 1) / kThreads, 8192));
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_CONCAT, s);
+  hipLaunchKernelGGL(concat_kernel, dim3(grid), dim3(kThreads), 0, s, pl, pr, out, C, D, H, W, total);
+  return finish_launch("fsmi_concat_volume");
+}
+
+int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, const float* Bm, const float* Wg,
+                          float* out, int B, int C, int G, int Cs, int D, int H, int W, void* stream) {
+  FSMI_CHECK_ARG(fl && fr && A && Bm && Wg && out, "fsmi_comb_volume_stem: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && Cs > 0 && D > 0 && H > 0 && W > 0, "fsmi_comb_volume_stem: bad shape");
+  FSMI_CHECK_ARG(G == 8, "fsmi_comb_volume_stem: num_groups must be 8 (cv_group), got %d", G);
+  FSMI_CHECK_ARG(C % G == 0, "C:%d, num_groups:%d", C, G);
+  const int Cg = C / G;
+  const size_t lds = (static_cast<size_t>(std::max(2 * Cg * W, 2 * Cs * W)) + Cs * G) * sizeof(float);
+  FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_comb_volume_stem: row too large for LDS (W=%d)", W);
+  const int DC = pick_dc(D, W);
+  const int nDC = (D + DC - 1) / DC;
+  const unsigned grid = static_cast<unsigned>(B) * H * nDC;
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_COMB, s);
+  hipLaunchKernelGGL((comb_stem_kernel<8, kNout>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs,
+                     D, H, W, DC, nDC);
+  return finish_launch("fsmi_comb_volume_stem");
+}
+
+int fsmi_pointwise_proj(const float* x, const float* Wt, const float* bias, float* out, int B, int C, int O, int H,
+                        int W, void* stream) {
+  FSMI_CHECK_ARG(x && Wt && out, "fsmi_pointwise_proj: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && O > 0 && H > 0 && W > 0, "fsmi_pointwise_proj: bad shape");
+  const int P = H * W;
+  dim3 grid(ceil_div(P, kThreads), ceil_div(O, kProjO), B);
+  const size_t lds = static_cast<size_t>(kProjO) * C * sizeof(float);
+  FSMI_CHECK_ARG(lds <= 64 * 1024, "fsmi_pointwise_proj: C=%d too large", C);
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_PROJ, s);
+  hipLaunchKernelGGL(proj_kernel, grid, dim3(kThreads), lds, s, x, Wt, bias, out, C, O, P);
+  return finish_launch("fsmi_pointwise_proj");
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+"""Context network and the backbone seam (``core/extractor.py``).
+
+The context path runs once per pair before the refinement loop and is OUT of
+the hot-path scope: it stays stock PyTorch-ROCm here, with
+the reference's module tree so checkpoints load.  The backbone (EdgeNeXt-S +
+DepthAnythingV2, ``Feature``) needs remote weights and is out of scope
+(SURVEY §2 row 9); ``SyntheticFeature`` stands in for it, returning
+device-resident feature maps with ``Feature.d_out`` channels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import synth
+from .submodule import BasicConv
+
+__all__ = ["ResidualBlock", "ContextNetDino", "DepthAnythingFeature", "SyntheticFeature"]
+
+
+class DepthAnythingFeature:
+    """Only the config table of core/extractor.py:286-291 (the ViT itself is out of scope)."""
+    model_configs = {
+        "vitl": {"encoder": "vitl", "features": 256, "out_channels": [256, 512, 1024, 1024]},
+        "vitb": {"encoder": "vitb", "features": 128, "out_channels": [96, 192, 384, 768]},
+        "vits": {"encoder": "vits", "features": 64, "out_channels": [48, 96, 192, 384]},
+    }
+
+
+class ResidualBlock(nn.Module):
+    """core/extractor.py:20-80 (batch / instance / none norms)."""
+
+    def __init__(self, in_planes, planes, norm_fn="group", stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, kernel_size=3, padding=1, stride=stride)
+        self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+        proj = not (stride == 1 and in_planes == planes)
+
+        def mk():
+            if norm_fn == "group":
+                return nn.GroupNorm(num_groups=planes // 8, num_channels=planes)
+            if norm_fn == "batch":
+                return nn.BatchNorm2d(planes)
+            if norm_fn == "instance":
+                return nn.InstanceNorm2d(planes)
+            return nn.Sequential()
+
+        self.norm1 = mk()
+        self.norm2 = mk()
+        if proj:
+            self.norm3 = mk()
+        self.downsample = nn.Sequential(nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride),
+                                        self.norm3) if proj else None
+
+    def forward(self, x):
+        y = F.relu(self.norm1(self.conv1(x)))
+        y = F.relu(self.norm2(self.conv2(y)))
+        if self.downsample is not None:
+            x = self.downsample(x)
+        return F.relu(x + y)
+
+
+class ContextNetDino(nn.Module):
+    """core/extractor.py:192-283 (norm_fn='batch')."""
+
+    def __init__(self, args, output_dim=[128], norm_fn="batch", downsample=3):
+        super().__init__()
+        self.args = args
+        self.patch_size = 14
+        self.image_size = 518
+        self.vit_feat_dim = 384
+        self.out_dims = output_dim
+        self.norm_fn = norm_fn
+        self.norm1 = nn.BatchNorm2d(64) if norm_fn == "batch" else nn.InstanceNorm2d(64)
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=1 + (downsample > 2), padding=3)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.in_planes = 64
+        self.layer1 = self._make_layer(64, stride=1)
+        self.layer2 = self._make_layer(96, stride=1 + (downsample > 1))
+        self.layer3 = self._make_layer(128, stride=1 + (downsample > 0))
+        self.layer4 = self._make_layer(128, stride=2)
+        self.layer5 = self._make_layer(128, stride=2)
+        self.down = nn.Sequential(nn.Conv2d(128, 128, kernel_size=4, stride=4, padding=0), nn.BatchNorm2d(128))
+        vit_dim = DepthAnythingFeature.model_configs[self.args.vit_size]["features"] // 2
+        self.conv2 = BasicConv(128 + vit_dim, 128, kernel_size=3, padding=1)
+        self.norm = nn.BatchNorm2d(256)
+        self.outputs04 = nn.ModuleList([nn.Sequential(ResidualBlock(128, 128, norm_fn, stride=1),
+                                                      nn.Conv2d(128, d[2], 3, padding=1)) for d in output_dim])
+        self.outputs08 = nn.ModuleList([nn.Sequential(ResidualBlock(128, 128, norm_fn, stride=1),
+                                                      nn.Conv2d(128, d[1], 3, padding=1)) for d in output_dim])
+        self.outputs16 = nn.ModuleList([nn.Conv2d(128, d[0], 3, padding=1) for d in output_dim])
+
+    def _make_layer(self, dim, stride=1):
+        layers = nn.Sequential(ResidualBlock(self.in_planes, dim, self.norm_fn, stride=stride),
+                               ResidualBlock(dim, dim, self.norm_fn, stride=1))
+        self.in_planes = dim
+        return layers
+
+    def forward(self, x_in, vit_feat, dual_inp=False, num_layers=3):
+        x = self.relu1(self.norm1(self.conv1(x_in)))
+        x = self.layer3(self.layer2(self.layer1(x)))
+        x = self.conv2(torch.cat([x, vit_feat], dim=1))
+        o4 = [f(x) for f in self.outputs04]
+        y = self.layer4(x)
+        o8 = [f(y) for f in self.outputs08]
+        z = self.layer5(y)
+        o16 = [f(z) for f in self.outputs16]
+        return o4, o8, o16
+
+
+class SyntheticFeature(nn.Module):
+    """Stand-in for ``Feature`` (core/extractor.py:323-369).
+
+    ``set_features(left, right, vit)`` installs device-resident feature maps
+    (the backbone output, already in HBM); ``forward`` returns them in the
+    reference's ``([x4, x8, x16, x32], vit_feat)`` form for the concatenated
+    ``[left; right]`` batch.  Without installed features it synthesises them
+    from ``synth.backbone_features`` for the image size (host-side; tests).
+    """
+
+    def __init__(self, args):
+        super().__init__()
+        self.args = args
+        self.d_out, self.vit_dim = synth.feature_dims(args.vit_size)
+        self._preset = None
+
+    def set_features(self, left, right, vit):
+        self._preset = (list(left), list(right), vit)
+
+    def forward(self, x):
+        if self._preset is None:
+            B2, _, H, W = x.shape
+            fl, fr, vit = synth.backbone_features(B2 // 2, H, W, self.args.vit_size)
+            left = [torch.from_numpy(a).to(x.device) for a in fl]
+            right = [torch.from_numpy(a).to(x.device) for a in fr]
+            vit = torch.from_numpy(vit).to(x.device)
+        else:
+            left, right, vit = self._preset
+        out = [torch.cat([a, b], 0) for a, b in zip(left, right)]
+        return out, torch.cat([vit, vit], 0)

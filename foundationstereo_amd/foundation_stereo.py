@@ -1,0 +1,244 @@
+"""FoundationStereo forward with the MI355X-native hot path (``core/foundation_stereo.py``).
+
+Module tree and ``state_dict`` keys are the reference's (checkpoints load
+unchanged; ``feature.*`` belongs to the out-of-scope backbone).  What changes
+is the data path:
+
+* a1+a2: gwc + concat + the 1x1x1 ``corr_stem[0]`` conv are ONE kernel
+  (``ops.comb_volume_stem``) writing the 28-channel stem volume directly --
+  the 32-channel comb volume and its cat copy never exist in HBM;
+* a3: 3D filtering on MIOpen (``torch.nn``);
+* a4: softmax + soft-argmin fused (``ops.softmax_regression``); skipped when an
+  ``init_disp`` is supplied (hierarchical pass) since the reference discards it;
+* a5/a6: geometry encoding + per-iteration lookup on HIP (``geometry.py``);
+* a7: ConvGRU with fused gates (``update.py``);
+* a9: softmax(9) + convex x4 upsampling fused (``ops.softmax_context_upsample``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .extractor import ContextNetDino, SyntheticFeature
+from .geometry import Combined_Geo_Encoding_Volume
+from .submodule import (BasicConv, BasicConv_IN, ChannelAttentionEnhancement, Conv2x, Conv3dNormActReduced,
+                        CostVolumeDisparityAttention, FeatureAtt, ResnetBasicBlock3D, SpatialAttentionExtractor,
+                        build_concat_volume, build_gwc_volume)
+from .update import BasicSelectiveMultiUpdateBlock
+from .utils import InputPadder
+
+_MEAN = (0.485, 0.456, 0.406)
+_STD = (0.229, 0.224, 0.225)
+
+
+def autocast(enabled):
+    return torch.autocast("cuda", dtype=torch.float16, enabled=bool(enabled))
+
+
+def normalize_image(img):
+    """(x/255 - mean)/std per RGB channel (core/foundation_stereo.py:37-42)."""
+    mean = torch.tensor(_MEAN, device=img.device, dtype=img.dtype).view(1, 3, 1, 1)
+    std = torch.tensor(_STD, device=img.device, dtype=img.dtype).view(1, 3, 1, 1)
+    return ((img / 255.0 - mean) / std).contiguous()
+
+
+class hourglass(nn.Module):
+    """3-level 3D hourglass with feature attention and the disparity transformer
+    (core/foundation_stereo.py:45-123)."""
+
+    def __init__(self, cfg, in_channels, feat_dims=None):
+        super().__init__()
+        self.cfg = cfg
+        c = in_channels
+
+        def down(ci, co):
+            return nn.Sequential(BasicConv(ci, co, is_3d=True, bn=True, relu=True, kernel_size=3, padding=1, stride=2,
+                                           dilation=1),
+                                 Conv3dNormActReduced(co, co, kernel_size=3, kernel_disp=17))
+
+        def up(ci, co):
+            return BasicConv(ci, co, deconv=True, is_3d=True, bn=True, relu=True, kernel_size=(4, 4, 4),
+                             padding=(1, 1, 1), stride=(2, 2, 2))
+
+        def agg(ci, co):
+            return nn.Sequential(BasicConv(ci, co, is_3d=True, kernel_size=1, padding=0, stride=1),
+                                 Conv3dNormActReduced(co, co, kernel_size=3, kernel_disp=17),
+                                 Conv3dNormActReduced(co, co, kernel_size=3, kernel_disp=17))
+
+        self.conv1 = down(c, 2 * c)
+        self.conv2 = down(2 * c, 4 * c)
+        self.conv3 = down(4 * c, 6 * c)
+        self.conv3_up = up(6 * c, 4 * c)
+        self.conv2_up = up(4 * c, 2 * c)
+        self.conv1_up = up(2 * c, c)
+        self.conv_out = nn.Sequential(Conv3dNormActReduced(c, c, kernel_size=3, kernel_disp=17),
+                                      Conv3dNormActReduced(c, c, kernel_size=3, kernel_disp=17))
+        self.agg_0 = agg(8 * c, 4 * c)
+        self.agg_1 = agg(4 * c, 2 * c)
+        self.atts = nn.ModuleDict({"4": CostVolumeDisparityAttention(d_model=c, nhead=4, dim_feedforward=c,
+                                                                     norm_first=False, num_transformer=4,
+                                                                     max_len=self.cfg["max_disp"] // 16)})
+        self.conv_patch = nn.Sequential(nn.Conv3d(c, c, kernel_size=4, stride=4, padding=0, groups=c),
+                                        nn.BatchNorm3d(c))
+        self.feature_att_8 = FeatureAtt(2 * c, feat_dims[1])
+        self.feature_att_16 = FeatureAtt(4 * c, feat_dims[2])
+        self.feature_att_32 = FeatureAtt(6 * c, feat_dims[3])
+        self.feature_att_up_16 = FeatureAtt(4 * c, feat_dims[2])
+        self.feature_att_up_8 = FeatureAtt(2 * c, feat_dims[1])
+
+    def forward(self, x, features):
+        c1 = self.feature_att_8(self.conv1(x), features[1])
+        c2 = self.feature_att_16(self.conv2(c1), features[2])
+        c3 = self.feature_att_32(self.conv3(c2), features[3])
+        c2 = self.feature_att_up_16(self.agg_0(torch.cat((self.conv3_up(c3), c2), dim=1)), features[2])
+        c1 = self.feature_att_up_8(self.agg_1(torch.cat((self.conv2_up(c2), c1), dim=1)), features[1])
+        conv = self.conv1_up(c1)
+        t = self.atts["4"](self.conv_patch(x))
+        conv = conv + F.interpolate(t, scale_factor=4, mode="trilinear", align_corners=False)
+        return self.conv_out(conv)
+
+
+class FoundationStereo(nn.Module):
+    """core/foundation_stereo.py:127-274 (minus the out-of-scope backbone)."""
+
+    def __init__(self, args, feature=None):
+        super().__init__()
+        self.args = args
+        context_dims = args.hidden_dims
+        self.cv_group = 8
+        volume_dim = 28
+        self.cnet = ContextNetDino(args, output_dim=[args.hidden_dims, context_dims], downsample=args.n_downsample)
+        self.update_block = BasicSelectiveMultiUpdateBlock(self.args, self.args.hidden_dims[0], volume_dim=volume_dim)
+        self.sam = SpatialAttentionExtractor()
+        self.cam = ChannelAttentionEnhancement(self.args.hidden_dims[0])
+        self.context_zqr_convs = nn.ModuleList([nn.Conv2d(context_dims[i], args.hidden_dims[i] * 3, kernel_size=3,
+                                                          padding=1) for i in range(self.args.n_gru_layers)])
+        self.feature = feature if feature is not None else SyntheticFeature(args)
+        self.proj_cmb = nn.Conv2d(self.feature.d_out[0], 12, kernel_size=1, padding=0)
+        self.stem_2 = nn.Sequential(BasicConv_IN(3, 32, kernel_size=3, stride=2, padding=1),
+                                    nn.Conv2d(32, 32, 3, 1, 1, bias=False), nn.InstanceNorm2d(32), nn.ReLU())
+        self.stem_4 = nn.Sequential(BasicConv_IN(32, 48, kernel_size=3, stride=2, padding=1),
+                                    nn.Conv2d(48, 48, 3, 1, 1, bias=False), nn.InstanceNorm2d(48), nn.ReLU())
+        self.spx_2_gru = Conv2x(32, 32, True, bn=False)
+        self.spx_gru = nn.Sequential(nn.ConvTranspose2d(2 * 32, 9, kernel_size=4, stride=2, padding=1))
+        self.corr_stem = nn.Sequential(
+            nn.Conv3d(32, volume_dim, kernel_size=1),
+            BasicConv(volume_dim, volume_dim, kernel_size=3, padding=1, is_3d=True),
+            ResnetBasicBlock3D(volume_dim, volume_dim, kernel_size=3, stride=1, padding=1),
+            ResnetBasicBlock3D(volume_dim, volume_dim, kernel_size=3, stride=1, padding=1))
+        self.corr_feature_att = FeatureAtt(volume_dim, self.feature.d_out[0])
+        self.cost_agg = hourglass(cfg=self.args, in_channels=volume_dim, feat_dims=self.feature.d_out)
+        self.classifier = nn.Sequential(
+            BasicConv(volume_dim, volume_dim // 2, kernel_size=3, padding=1, is_3d=True),
+            ResnetBasicBlock3D(volume_dim // 2, volume_dim // 2, kernel_size=3, stride=1, padding=1),
+            nn.Conv3d(volume_dim // 2, 1, kernel_size=7, padding=3))
+        r = self.args.corr_radius
+        self.dx = torch.linspace(-r, r, 2 * r + 1, requires_grad=False).reshape(1, 1, 2 * r + 1, 1)
+        self.fused_volume = True
+        self._stem_cache = None
+
+    # ------------------------------------------------------------ volume build
+    def _stem_weights(self):
+        """Fold proj_cmb into the concat columns of corr_stem[0] (exact algebra, fp64)."""
+        stem, proj = self.corr_stem[0], self.proj_cmb
+        key = tuple((t.data_ptr(), t._version) for t in (stem.weight, stem.bias, proj.weight, proj.bias))
+        if self._stem_cache is None or self._stem_cache[0] != key:
+            with torch.no_grad():
+                S = stem.weight.reshape(stem.weight.shape[0], -1).double()       # (Cs, 32)
+                sb = stem.bias.double()
+                P = proj.weight.reshape(proj.weight.shape[0], -1).double()        # (12, C)
+                pb = proj.bias.double()
+                G = self.cv_group
+                Sl, Sr = S[:, G:G + 12], S[:, G + 12:G + 24]
+                wa, ba = Sl @ P, Sl @ pb + sb
+                wb, bb = Sr @ P, Sr @ pb
+                tensors = [t.float().contiguous() for t in (S[:, :G], wa, ba, wb, bb)]
+            self._stem_cache = (key, tensors)
+        return self._stem_cache[1]
+
+    def build_stem_volume(self, fl0, fr0):
+        """gwc + concat + corr_stem[0] -> (B, 28, D4, H4, W4) (core/foundation_stereo.py:207-213)."""
+        D4 = self.args["max_disp"] // 4
+        fl0, fr0 = fl0.float(), fr0.float()
+        if not self.fused_volume:
+            gwc = build_gwc_volume(fl0, fr0, D4, self.cv_group)
+            cat = build_concat_volume(self.proj_cmb(fl0), self.proj_cmb(fr0), D4)
+            return self.corr_stem[0](torch.cat([gwc, cat], dim=1))
+        wg, wa, ba, wb, bb = self._stem_weights()
+        A = ops.pointwise_proj(fl0, wa, ba)
+        Bm = ops.pointwise_proj(fr0, wb, bb)
+        return ops.comb_volume_stem(fl0, fr0, A, Bm, wg, D4)
+
+    def _backbone(self, image1, image2):
+        B = len(image1)
+        out, vit_feat = self.feature(torch.cat([image1, image2], dim=0))
+        return [o[:B] for o in out], [o[B:] for o in out], vit_feat[:B]
+
+    def upsample_disp(self, disp, mask_feat_4, stem_2x):
+        """core/foundation_stereo.py:183-191: returns (B,1,H,W) fp32."""
+        with autocast(self.args.mixed_precision):
+            xspx = self.spx_2_gru(mask_feat_4, stem_2x)
+            logits = self.spx_gru(xspx)
+        return ops.softmax_context_upsample(disp.float(), logits.float(), 4.0).unsqueeze(1)
+
+    def forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):
+        B = len(image1)
+        image1 = normalize_image(image1)
+        image2 = normalize_image(image2)
+        mp = self.args.mixed_precision
+        with autocast(mp):
+            features_left, features_right, vit_feat = self._backbone(image1, image2)
+            stem_2x = self.stem_2(image1)
+            vol = self.build_stem_volume(features_left[0], features_right[0])
+            vol = self.corr_stem[1:](vol)
+            vol = self.corr_feature_att(vol, features_left[0])
+            vol = self.cost_agg(vol, features_left)
+            if init_disp is None:
+                logits = self.classifier(vol).squeeze(1)
+                init_disp = ops.softmax_regression(logits.float())
+            cnet_list = self.cnet(image1, vit_feat=vit_feat, num_layers=self.args.n_gru_layers)
+            net_list = [torch.tanh(x[0]) for x in cnet_list]
+            inp_list = [torch.relu(x[1]) for x in cnet_list]
+            inp_list = [self.cam(x) * x for x in inp_list]
+            att = [self.sam(x) for x in inp_list]
+
+        geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
+                                              num_levels=self.args.corr_levels, dx=self.dx)
+        disp = init_disp.float()
+        disp_preds = []
+        disp_up = None
+        for itr in range(iters):
+            disp = disp.detach()
+            geo_feat = geo_fn(disp)
+            with autocast(mp):
+                net_list, mask_feat_4, delta_disp = self.update_block(net_list, inp_list, geo_feat, disp, att)
+            disp = disp + delta_disp.float()
+            if test_mode and itr < iters - 1:
+                continue
+            disp_up = self.upsample_disp(disp, mask_feat_4, stem_2x)
+            disp_preds.append(disp_up)
+        if test_mode:
+            return disp_up
+        return init_disp, disp_preds
+
+    def run_hierachical(self, image1, image2, iters=12, test_mode=False, low_memory=False, small_ratio=0.5):
+        """Coarse-to-fine driver (core/foundation_stereo.py:257-274), including the
+        reference's ``+= padder._pad[0]`` on the upsampled init."""
+        B, _, H, W = image1.shape
+        img1_small = F.interpolate(image1, scale_factor=small_ratio, align_corners=False, mode="bilinear")
+        img2_small = F.interpolate(image2, scale_factor=small_ratio, align_corners=False, mode="bilinear")
+        padder = InputPadder(img1_small.shape[-2:], divis_by=32, force_square=False)
+        img1_small, img2_small = padder.pad(img1_small, img2_small)
+        disp_small = self.forward(img1_small, img2_small, test_mode=True, iters=iters, low_memory=low_memory)
+        disp_small = padder.unpad(disp_small.float())
+        disp_small_up = F.interpolate(disp_small, size=(H, W), mode="bilinear", align_corners=True) * 1 / small_ratio
+        disp_small_up = disp_small_up.clip(0, None)
+        padder = InputPadder(image1.shape[-2:], divis_by=32, force_square=False)
+        image1, image2, disp_small_up = padder.pad(image1, image2, disp_small_up)
+        disp_small_up += padder._pad[0]
+        init_disp = F.interpolate(disp_small_up, scale_factor=0.25, mode="bilinear", align_corners=True) * 0.25
+        disp = self.forward(image1, image2, iters=iters, test_mode=test_mode, low_memory=low_memory,
+                            init_disp=init_disp)
+        return padder.unpad(disp.float())

@@ -1,0 +1,253 @@
+"""Torch-tensor front end of the HIP hot path (libfsmi.so, include/fsmi.h).
+
+Each op takes ROCm-resident fp32 tensors, allocates its output through the
+PyTorch caching allocator, and launches on the current HIP stream -- no host
+synchronisation, so a whole refinement loop can be captured in a hipGraph.
+There is no CPU path: CPU tensors raise (the CPU restatement lives in the
+test-only ``oracle`` package).  The ops are inference-only (the reference's
+training backprop is out of scope): inputs that require grad
+while grad mode is on raise.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+
+from . import _lib
+
+Tensor = torch.Tensor
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(name: str, *ts: Tensor):
+    for t in ts:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name}: expected tensors")
+        if not t.is_cuda:
+            raise RuntimeError(f"{name}: fsmi ops run on ROCm (HIP) device tensors only; got {t.device}")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"{name}: expected float32, got {t.dtype}")
+        if torch.is_grad_enabled() and t.requires_grad:
+            raise RuntimeError(f"{name}: fsmi ops are inference-only (input requires grad)")
+
+
+def _c(t: Tensor) -> Tensor:
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _p(t: Tensor) -> int:
+    return t.data_ptr()
+
+
+# ---------------------------------------------------------------- cost volume
+
+def gwc_volume(fl: Tensor, fr: Tensor, maxdisp: int, num_groups: int) -> Tensor:
+    """core/submodule.py:399-412 -> (B,G,D,H,W)."""
+    _check("gwc_volume", fl, fr)
+    B, C, H, W = fl.shape
+    assert C % num_groups == 0, f"C:{C}, num_groups:{num_groups}"
+    fl, fr = _c(fl), _c(fr)
+    out = torch.empty((B, num_groups, maxdisp, H, W), device=fl.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_gwc_volume(_p(fl), _p(fr), _p(out), B, C, num_groups, maxdisp, H, W,
+                                           _stream(fl)), "gwc_volume")
+    return out
+
+
+def concat_volume(pl: Tensor, pr: Tensor, maxdisp: int) -> Tensor:
+    """core/submodule.py:416-427 -> (B,2C,D,H,W)."""
+    _check("concat_volume", pl, pr)
+    B, C, H, W = pl.shape
+    pl, pr = _c(pl), _c(pr)
+    out = torch.empty((B, 2 * C, maxdisp, H, W), device=pl.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_concat_volume(_p(pl), _p(pr), _p(out), B, C, maxdisp, H, W, _stream(pl)),
+               "concat_volume")
+    return out
+
+
+def pointwise_proj(x: Tensor, wt: Tensor, bias: Tensor = None) -> Tensor:
+    """out[b,o] = bias[o] + sum_c wt[o,c] x[b,c]  (1x1 conv)."""
+    _check("pointwise_proj", x, wt, *([bias] if bias is not None else []))
+    B, C, H, W = x.shape
+    O = wt.shape[0]
+    x, wt = _c(x), _c(wt)
+    out = torch.empty((B, O, H, W), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_pointwise_proj(_p(x), _p(wt), _p(bias) if bias is not None else None, _p(out),
+                                               B, C, O, H, W, _stream(x)), "pointwise_proj")
+    return out
+
+
+def comb_volume_stem(fl: Tensor, fr: Tensor, A: Tensor, Bm: Tensor, Wg: Tensor, maxdisp: int) -> Tensor:
+    """Fused gwc + concat + corr_stem[0] (core/foundation_stereo.py:207-213,165) -> (B,Cs,D,H,W)."""
+    _check("comb_volume_stem", fl, fr, A, Bm, Wg)
+    B, C, H, W = fl.shape
+    Cs, G = Wg.shape
+    assert C % G == 0, f"C:{C}, num_groups:{G}"
+    fl, fr, A, Bm, Wg = _c(fl), _c(fr), _c(A), _c(Bm), _c(Wg)
+    out = torch.empty((B, Cs, maxdisp, H, W), device=fl.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_comb_volume_stem(_p(fl), _p(fr), _p(A), _p(Bm), _p(Wg), _p(out), B, C, G, Cs,
+                                                 maxdisp, H, W, _stream(fl)), "comb_volume_stem")
+    return out
+
+
+# ---------------------------------------------------------------- geometry
+
+def allpairs_corr(fl: Tensor, fr: Tensor, num_levels: int) -> List[Tensor]:
+    """core/geometry.py:24-40,68-77 -> [(B,H,W,W_i)] with W_i = W >> i."""
+    _check("allpairs_corr", fl, fr)
+    B, C, H, W = fl.shape
+    fl, fr = _c(fl), _c(fr)
+    levels = [torch.empty((B, H, W, W >> i), device=fl.device, dtype=torch.float32) for i in range(num_levels)]
+    pp, keep = _lib.ptr_array([_p(t) for t in levels])
+    _lib.check(_lib.load().fsmi_allpairs_corr(_p(fl), _p(fr), pp, num_levels, B, C, H, W, _stream(fl)),
+               "allpairs_corr")
+    del keep
+    return levels
+
+
+def volume_pyramid(vol: Tensor, num_levels: int) -> List[Tensor]:
+    """core/geometry.py:29,34-36 in the native (B,Cv,D,H,W) layout -> [vol, lvl1, ...]."""
+    _check("volume_pyramid", vol)
+    B, Cv, D, H, W = vol.shape
+    vol = _c(vol)
+    levels = [torch.empty((B, Cv, D >> i, H, W), device=vol.device, dtype=torch.float32)
+              for i in range(1, num_levels)]
+    if levels:
+        pp, keep = _lib.ptr_array([_p(t) for t in levels])
+        _lib.check(_lib.load().fsmi_volume_pyramid(_p(vol), pp, num_levels, B, Cv, D, H, W, _stream(vol)),
+                   "volume_pyramid")
+        del keep
+    return [vol] + levels
+
+
+def geo_lookup(vol_levels: Sequence[Tensor], corr_levels: Sequence[Tensor], disp: Tensor, radius: int,
+               out: Tensor = None) -> Tensor:
+    """core/geometry.py:43-65 -> (B, L*(2r+1)*(Cv+1), H, W)."""
+    _check("geo_lookup", disp, *vol_levels, *corr_levels)
+    L = len(vol_levels)
+    B, Cv, D, H, W = vol_levels[0].shape
+    W2 = corr_levels[0].shape[-1]
+    assert disp.shape == (B, 1, H, W), f"disp {tuple(disp.shape)} vs volume {(B, 1, H, W)}"
+    for i in range(L):
+        assert vol_levels[i].shape == (B, Cv, D >> i, H, W) and vol_levels[i].is_contiguous()
+        assert corr_levels[i].shape == (B, H, W, W2 >> i) and corr_levels[i].is_contiguous()
+    disp = _c(disp)
+    K = 2 * radius + 1
+    if out is None:
+        out = torch.empty((B, L * K * (Cv + 1), H, W), device=disp.device, dtype=torch.float32)
+    pv, kv = _lib.ptr_array([_p(t) for t in vol_levels])
+    pc, kc = _lib.ptr_array([_p(t) for t in corr_levels])
+    _lib.check(_lib.load().fsmi_geo_lookup(pv, pc, _p(disp), _p(out), L, radius, B, Cv, D, H, W, W2,
+                                           _stream(disp)), "geo_lookup")
+    del kv, kc
+    return out
+
+
+def bilinear_sampler_1d(img: Tensor, x: Tensor) -> Tensor:
+    """core/utils/utils.py:44-55 (H == 1): img (P,C,1,Lx), x (P,K) -> (P,C,1,K)."""
+    _check("bilinear_sampler", img, x)
+    P, C, Hh, Lx = img.shape
+    assert Hh == 1
+    K = x.shape[-1]
+    img, x = _c(img), _c(x.reshape(P, K))
+    out = torch.empty((P, C, 1, K), device=img.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_bilinear_sampler_1d(_p(img), _p(x), _p(out), P, C, Lx, K, _stream(img)),
+               "bilinear_sampler")
+    return out
+
+
+# ---------------------------------------------------------------- heads
+
+def disparity_regression(prob: Tensor, maxdisp: int) -> Tensor:
+    """core/submodule.py:431-435."""
+    assert len(prob.shape) == 4
+    _check("disparity_regression", prob)
+    B, D, H, W = prob.shape
+    assert D == maxdisp
+    prob = _c(prob)
+    out = torch.empty((B, 1, H, W), device=prob.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_disparity_regression(_p(prob), _p(out), B, D, H, W, _stream(prob)),
+               "disparity_regression")
+    return out
+
+
+def softmax_regression(logits: Tensor) -> Tensor:
+    """softmax over D then disparity_regression (core/foundation_stereo.py:218-220)."""
+    _check("softmax_regression", logits)
+    B, D, H, W = logits.shape
+    logits = _c(logits)
+    out = torch.empty((B, 1, H, W), device=logits.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_softmax_regression(_p(logits), _p(out), B, D, H, W, _stream(logits)),
+               "softmax_regression")
+    return out
+
+
+def context_upsample(disp_low: Tensor, up_weights: Tensor) -> Tensor:
+    """core/submodule.py:456-468 -> (B,4h,4w)."""
+    _check("context_upsample", disp_low, up_weights)
+    b, c, h, w = disp_low.shape
+    assert c == 1 and up_weights.shape == (b, 9, 4 * h, 4 * w)
+    disp_low, up_weights = _c(disp_low), _c(up_weights)
+    out = torch.empty((b, 4 * h, 4 * w), device=disp_low.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_context_upsample(_p(disp_low), _p(up_weights), _p(out), b, h, w,
+                                                 _stream(disp_low)), "context_upsample")
+    return out
+
+
+def softmax_context_upsample(disp_low: Tensor, logits: Tensor, scale: float = 4.0) -> Tensor:
+    """softmax(9) + context_upsample(scale*disp) fused (core/foundation_stereo.py:187-189) -> (B,4h,4w)."""
+    _check("softmax_context_upsample", disp_low, logits)
+    b, c, h, w = disp_low.shape
+    assert c == 1 and logits.shape == (b, 9, 4 * h, 4 * w)
+    disp_low, logits = _c(disp_low), _c(logits)
+    out = torch.empty((b, 4 * h, 4 * w), device=disp_low.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_softmax_context_upsample(_p(disp_low), _p(logits), _p(out), float(scale), b, h, w,
+                                                         _stream(disp_low)), "softmax_context_upsample")
+    return out
+
+
+def gru_reset(zr_s: Tensor, zr_l: Tensor, h: Tensor, x: Tensor):
+    """[sigmoid(r)*h, x] for the small and large GRU (core/update.py:92-93)."""
+    _check("gru_reset", zr_s, zr_l, h, x)
+    B, Hd, H, W = h.shape
+    Cx = x.shape[1]
+    zr_s, zr_l, h, x = _c(zr_s), _c(zr_l), _c(h), _c(x)
+    qs = torch.empty((B, Hd + Cx, H, W), device=h.device, dtype=torch.float32)
+    ql = torch.empty_like(qs)
+    _lib.check(_lib.load().fsmi_gru_reset(_p(zr_s), _p(zr_l), _p(h), _p(x), _p(qs), _p(ql), B, Hd, Cx, H, W,
+                                          _stream(h)), "gru_reset")
+    return qs, ql
+
+
+def gru_blend(zr_s: Tensor, zr_l: Tensor, q_s: Tensor, q_l: Tensor, h: Tensor, att: Tensor) -> Tensor:
+    """att*GRU_small + (1-att)*GRU_large state update (core/update.py:91,94-95,117)."""
+    _check("gru_blend", zr_s, zr_l, q_s, q_l, h, att)
+    B, Hd, H, W = h.shape
+    zr_s, zr_l, q_s, q_l, h, att = (_c(t) for t in (zr_s, zr_l, q_s, q_l, h, att))
+    out = torch.empty_like(h)
+    _lib.check(_lib.load().fsmi_gru_blend(_p(zr_s), _p(zr_l), _p(q_s), _p(q_l), _p(h), _p(att), _p(out), B, Hd,
+                                          H, W, _stream(h)), "gru_blend")
+    return out
+
+
+# ---------------------------------------------------------------- timing
+
+def timer_enable(on: bool = True):
+    _lib.check(_lib.load().fsmi_timer_enable(1 if on else 0), "timer_enable")
+
+
+def timer_reset():
+    _lib.check(_lib.load().fsmi_timer_reset(), "timer_reset")
+
+
+def timer_query(kernel: str):
+    """(total_ms, launches) of ``kernel`` since the last reset (synchronises its events)."""
+    import ctypes
+    tot = ctypes.c_double(0.0)
+    cnt = ctypes.c_longlong(0)
+    _lib.check(_lib.load().fsmi_timer_query(_lib.KERNELS.index(kernel), ctypes.byref(tot), ctypes.byref(cnt)),
+               "timer_query")
+    return tot.value, cnt.value

@@ -1,0 +1,413 @@
+"""Drop-in for ``core/submodule.py``: cost-volume functions on HIP, 3D filtering blocks.
+
+Public names and module trees (hence ``state_dict`` keys) match the reference
+so ``core.foundation_stereo`` can star-import this module instead
+(SURVEY §8b).  The cost-volume functions, ``disparity_regression`` and
+``context_upsample`` run the hand-written gfx950 kernels of ``libfsmi.so``;
+dense convolutions stay on MIOpen through ``torch.nn``.
+
+The disparity transformer's attention uses PyTorch SDPA in place of the
+reference's third-party ``flash_attn_func`` (core/submodule.py:224): same
+non-causal softmax(QK^T/sqrt(d))V math.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+__all__ = [
+    "LayerNorm2d", "BasicConv", "Conv3dNormActReduced", "ResnetBasicBlock", "ResnetBasicBlock3D",
+    "FlashMultiheadAttention", "FlashAttentionTransformerEncoderLayer", "UpsampleConv", "Conv2x",
+    "BasicConv_IN", "Conv2x_IN", "groupwise_correlation", "build_gwc_volume", "build_concat_volume",
+    "disparity_regression", "FeatureAtt", "context_upsample", "PositionalEmbedding",
+    "CostVolumeDisparityAttention", "ChannelAttentionEnhancement", "SpatialAttentionExtractor",
+    "EdgeNextConvEncoder",
+]
+
+_leaky = nn.LeakyReLU()  # slope 0.01, as the reference's nn.LeakyReLU() (core/submodule.py:85)
+
+
+class LayerNorm2d(nn.LayerNorm):
+    """Channels-first LayerNorm (core/submodule.py:29-47)."""
+
+    def __init__(self, normalized_shape, eps=1e-6):
+        super().__init__(normalized_shape, eps=eps)
+
+    def forward(self, x):
+        y = F.layer_norm(x.permute(0, 2, 3, 1), self.normalized_shape, self.weight, self.bias, self.eps)
+        return y.permute(0, 3, 1, 2).contiguous()
+
+
+def _norm(kind, ch, is_3d):
+    if kind == "batch":
+        return nn.BatchNorm3d(ch) if is_3d else nn.BatchNorm2d(ch)
+    return nn.InstanceNorm3d(ch) if is_3d else nn.InstanceNorm2d(ch)
+
+
+class BasicConv(nn.Module):
+    """conv (no bias) -> BN/IN -> LeakyReLU(0.01)  (core/submodule.py:51-86)."""
+
+    def __init__(self, in_channels, out_channels, deconv=False, is_3d=False, bn=True, relu=True, norm="batch",
+                 **kwargs):
+        super().__init__()
+        self.relu = relu
+        self.use_bn = bn
+        self.bn = nn.Identity()
+        conv_t = {(False, False): nn.Conv2d, (False, True): nn.ConvTranspose2d,
+                  (True, False): nn.Conv3d, (True, True): nn.ConvTranspose3d}[(is_3d, deconv)]
+        self.conv = conv_t(in_channels, out_channels, bias=False, **kwargs)
+        if bn:
+            self.bn = _norm(norm, out_channels, is_3d)
+
+    def forward(self, x):
+        x = self.bn(self.conv(x)) if self.use_bn else self.conv(x)
+        return F.leaky_relu(x, 0.01) if self.relu else x
+
+
+class Conv3dNormActReduced(nn.Module):
+    """Axial-planar conv: (1,k,k)+BN+ReLU then (kd,1,1)+BN+ReLU (core/submodule.py:89-114)."""
+
+    def __init__(self, C_in, C_out, hidden=None, kernel_size=3, kernel_disp=None, stride=1, norm=nn.BatchNorm3d):
+        super().__init__()
+        kd = kernel_size if kernel_disp is None else kernel_disp
+        hidden = C_out if hidden is None else hidden
+        k = kernel_size
+        self.conv1 = nn.Sequential(
+            nn.Conv3d(C_in, hidden, kernel_size=(1, k, k), padding=(0, k // 2, k // 2), stride=(1, stride, stride)),
+            norm(hidden), nn.ReLU())
+        self.conv2 = nn.Sequential(
+            nn.Conv3d(hidden, C_out, kernel_size=(kd, 1, 1), padding=(kd // 2, 0, 0), stride=(stride, 1, 1)),
+            norm(C_out), nn.ReLU())
+
+    def forward(self, x):
+        return self.conv2(self.conv1(x))
+
+
+class _ResBlock(nn.Module):
+    _conv = nn.Conv2d
+    _bn = nn.BatchNorm2d
+
+    def __init__(self, inplanes, planes, kernel_size=3, stride=1, padding=1, downsample=None, groups=1,
+                 base_width=64, dilation=1, norm_layer="default", bias=False):
+        super().__init__()
+        norm_layer = self._bn if norm_layer == "default" else norm_layer
+        if groups != 1 or base_width != 64:
+            raise ValueError("BasicBlock only supports groups=1 and base_width=64")
+        if dilation > 1:
+            raise NotImplementedError("Dilation > 1 not supported in BasicBlock")
+        self.norm_layer = norm_layer
+        self.conv1 = self._conv(inplanes, planes, kernel_size=kernel_size, stride=stride, bias=bias, padding=padding)
+        if norm_layer is not None:
+            self.bn1 = norm_layer(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = self._conv(planes, planes, kernel_size=kernel_size, stride=stride, bias=bias, padding=padding)
+        if norm_layer is not None:
+            self.bn2 = norm_layer(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        y = self.conv1(x)
+        if self.norm_layer is not None:
+            y = self.bn1(y)
+        y = F.relu(y)
+        y = self.conv2(y)
+        if self.norm_layer is not None:
+            y = self.bn2(y)
+        skip = x if self.downsample is None else self.downsample(x)
+        return F.relu(y + skip)
+
+
+class ResnetBasicBlock(_ResBlock):
+    """core/submodule.py:119-156."""
+
+
+class ResnetBasicBlock3D(_ResBlock):
+    """core/submodule.py:159-195."""
+    _conv = nn.Conv3d
+    _bn = nn.BatchNorm3d
+
+
+class FlashMultiheadAttention(nn.Module):
+    """core/submodule.py:198-229 with SDPA as the attention kernel."""
+
+    def __init__(self, embed_dim, num_heads):
+        super().__init__()
+        self.num_heads = num_heads
+        self.embed_dim = embed_dim
+        self.head_dim = embed_dim // num_heads
+        assert self.head_dim * num_heads == self.embed_dim, "embed_dim must be divisible by num_heads"
+        self.q_proj = nn.Linear(embed_dim, embed_dim)
+        self.k_proj = nn.Linear(embed_dim, embed_dim)
+        self.v_proj = nn.Linear(embed_dim, embed_dim)
+        self.out_proj = nn.Linear(embed_dim, embed_dim)
+
+    def forward(self, query, key, value, attn_mask=None, window_size=(-1, -1)):
+        B, L, C = query.shape
+
+        def heads(t):
+            return t.view(B, -1, self.num_heads, self.head_dim).transpose(1, 2)
+
+        o = F.scaled_dot_product_attention(heads(self.q_proj(query)), heads(self.k_proj(key)),
+                                           heads(self.v_proj(value)))
+        return self.out_proj(o.transpose(1, 2).reshape(B, L, C))
+
+
+class FlashAttentionTransformerEncoderLayer(nn.Module):
+    """Post-norm encoder layer (core/submodule.py:233-257); dropout is identity in eval."""
+
+    def __init__(self, embed_dim, num_heads, dim_feedforward, dropout=0.1, act=nn.GELU, norm=nn.LayerNorm):
+        super().__init__()
+        self.self_attn = FlashMultiheadAttention(embed_dim, num_heads)
+        self.act = act()
+        self.linear1 = nn.Linear(embed_dim, dim_feedforward)
+        self.dropout = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(dim_feedforward, embed_dim)
+        self.norm1 = norm(embed_dim)
+        self.norm2 = norm(embed_dim)
+        self.dropout1 = nn.Dropout(dropout)
+        self.dropout2 = nn.Dropout(dropout)
+
+    def forward(self, src, src_mask=None, window_size=(-1, -1)):
+        src = self.norm1(src + self.dropout1(self.self_attn(src, src, src, src_mask, window_size=window_size)))
+        ff = self.linear2(self.dropout(self.act(self.linear1(src))))
+        return self.norm2(src + self.dropout2(ff))
+
+
+class UpsampleConv(nn.Module):
+    """core/submodule.py:261-277."""
+
+    def __init__(self, C_in, C_out, is_3d=False, kernel_size=3, bias=True, stride=1, padding=1):
+        super().__init__()
+        self.is_3d = is_3d
+        conv = nn.Conv3d if is_3d else nn.Conv2d
+        self.conv = conv(C_in, C_out, kernel_size=kernel_size, stride=1, padding=kernel_size // 2, bias=bias)
+
+    def forward(self, x):
+        mode = "trilinear" if self.is_3d else "bilinear"
+        return self.conv(F.interpolate(x, scale_factor=2, align_corners=False, mode=mode))
+
+
+class Conv2x(nn.Module):
+    """core/submodule.py:281-317."""
+
+    def __init__(self, in_channels, out_channels, deconv=False, is_3d=False, concat=True, keep_concat=True, bn=True,
+                 relu=True, keep_dispc=False):
+        super().__init__()
+        self.concat = concat
+        self.is_3d = is_3d
+        kernel = (4, 4, 4) if (deconv and is_3d) else (4 if deconv else 3)
+        if deconv and is_3d and keep_dispc:
+            self.conv1 = BasicConv(in_channels, out_channels, deconv, is_3d, bn=bn, relu=True, kernel_size=(1, 4, 4),
+                                   stride=(1, 2, 2), padding=(0, 1, 1))
+        else:
+            self.conv1 = BasicConv(in_channels, out_channels, deconv, is_3d, bn=bn, relu=True, kernel_size=kernel,
+                                   stride=2, padding=1)
+        if concat:
+            mul = 2 if keep_concat else 1
+            self.conv2 = BasicConv(out_channels * 2, out_channels * mul, False, is_3d, bn, relu, kernel_size=3,
+                                   stride=1, padding=1)
+        else:
+            self.conv2 = BasicConv(out_channels, out_channels, False, is_3d, bn, relu, kernel_size=3, stride=1,
+                                   padding=1)
+
+    def forward(self, x, rem):
+        x = self.conv1(x)
+        if x.shape != rem.shape:
+            x = F.interpolate(x, size=(rem.shape[-2], rem.shape[-1]), mode="bilinear")
+        x = torch.cat((x, rem), 1) if self.concat else x + rem
+        return self.conv2(x)
+
+
+class BasicConv_IN(nn.Module):
+    """conv -> InstanceNorm -> LeakyReLU (core/submodule.py:320-346)."""
+
+    def __init__(self, in_channels, out_channels, deconv=False, is_3d=False, IN=True, relu=True, **kwargs):
+        super().__init__()
+        self.relu = relu
+        self.use_in = IN
+        conv_t = {(False, False): nn.Conv2d, (False, True): nn.ConvTranspose2d,
+                  (True, False): nn.Conv3d, (True, True): nn.ConvTranspose3d}[(is_3d, deconv)]
+        self.conv = conv_t(in_channels, out_channels, bias=False, **kwargs)
+        self.IN = nn.InstanceNorm3d(out_channels) if is_3d else nn.InstanceNorm2d(out_channels)
+
+    def forward(self, x):
+        x = self.conv(x)
+        if self.use_in:
+            x = self.IN(x)
+        return F.leaky_relu(x, 0.01) if self.relu else x
+
+
+class Conv2x_IN(nn.Module):
+    """core/submodule.py:349-385."""
+
+    def __init__(self, in_channels, out_channels, deconv=False, is_3d=False, concat=True, keep_concat=True, IN=True,
+                 relu=True, keep_dispc=False):
+        super().__init__()
+        self.concat = concat
+        self.is_3d = is_3d
+        kernel = (4, 4, 4) if (deconv and is_3d) else (4 if deconv else 3)
+        if deconv and is_3d and keep_dispc:
+            self.conv1 = BasicConv_IN(in_channels, out_channels, deconv, is_3d, IN=True, relu=True,
+                                      kernel_size=(1, 4, 4), stride=(1, 2, 2), padding=(0, 1, 1))
+        else:
+            self.conv1 = BasicConv_IN(in_channels, out_channels, deconv, is_3d, IN=True, relu=True,
+                                      kernel_size=kernel, stride=2, padding=1)
+        if concat:
+            mul = 2 if keep_concat else 1
+            self.conv2 = ResnetBasicBlock(out_channels * 2, out_channels * mul, kernel_size=3, stride=1, padding=1,
+                                          norm_layer=nn.InstanceNorm2d)
+        else:
+            self.conv2 = BasicConv_IN(out_channels, out_channels, False, is_3d, IN, relu, kernel_size=3, stride=1,
+                                      padding=1)
+
+    def forward(self, x, rem):
+        x = self.conv1(x)
+        if x.shape != rem.shape:
+            x = F.interpolate(x, size=(rem.shape[-2], rem.shape[-1]), mode="bilinear")
+        x = torch.cat((x, rem), 1) if self.concat else x + rem
+        return self.conv2(x)
+
+
+# ---------------------------------------------------------------- HIP hot path
+
+def groupwise_correlation(fea1, fea2, num_groups):
+    """core/submodule.py:388-397: the d=0 slice of the gwc volume, (B,G,H,W)."""
+    B, C, H, W = fea1.shape
+    assert C % num_groups == 0, f"C:{C}, num_groups:{num_groups}"
+    return ops.gwc_volume(fea1.float(), fea2.float(), 1, num_groups)[:, :, 0]
+
+
+def build_gwc_volume(refimg_fea, targetimg_fea, maxdisp, num_groups, stride=1):
+    """core/submodule.py:399-412 on the gfx950 kernel; fp32 out (the reference
+    computes the correlation in fp32 and stores it in the input dtype)."""
+    out = ops.gwc_volume(refimg_fea.float(), targetimg_fea.float(), maxdisp, num_groups)
+    return out if refimg_fea.dtype == torch.float32 else out.to(refimg_fea.dtype)
+
+
+def build_concat_volume(refimg_fea, targetimg_fea, maxdisp):
+    """core/submodule.py:416-427 on the gfx950 kernel."""
+    out = ops.concat_volume(refimg_fea.float(), targetimg_fea.float(), maxdisp)
+    return out if refimg_fea.dtype == torch.float32 else out.to(refimg_fea.dtype)
+
+
+def disparity_regression(x, maxdisp):
+    """core/submodule.py:431-435."""
+    assert len(x.shape) == 4
+    out = ops.disparity_regression(x.float(), maxdisp)
+    return out if x.dtype == torch.float32 else out.to(x.dtype)
+
+
+def context_upsample(disp_low, up_weights):
+    """core/submodule.py:456-468."""
+    return ops.context_upsample(disp_low.float(), up_weights.float())
+
+
+class FeatureAtt(nn.Module):
+    """sigmoid(conv1x1(LReLU(BN(conv1x1 feat)))) * cv  (core/submodule.py:438-454)."""
+
+    def __init__(self, cv_chan, feat_chan):
+        super().__init__()
+        self.feat_att = nn.Sequential(BasicConv(feat_chan, feat_chan // 2, kernel_size=1, stride=1, padding=0),
+                                      nn.Conv2d(feat_chan // 2, cv_chan, 1))
+
+    def forward(self, cv, feat):
+        return torch.sigmoid(self.feat_att(feat)).unsqueeze(2) * cv
+
+
+class PositionalEmbedding(nn.Module):
+    """Fixed sin/cos table (core/submodule.py:472-502); not a buffer, as in the reference."""
+
+    def __init__(self, d_model, max_len=512):
+        super().__init__()
+        pos = torch.arange(0, max_len).float().unsqueeze(1)
+        div = (torch.arange(0, d_model, 2).float() * -(math.log(10000.0) / d_model)).exp()[None]
+        pe = torch.zeros(max_len, d_model)
+        pe[:, 0::2] = torch.sin(pos * div)
+        pe[:, 1::2] = torch.cos(pos * div)
+        self.pe = pe.unsqueeze(0)
+
+    def forward(self, x, resize_embed=False):
+        self.pe = self.pe.to(x.device).to(x.dtype)
+        pe = self.pe
+        if pe.shape[1] < x.shape[1]:
+            if not resize_embed:
+                raise RuntimeError(f"x:{x.shape}, pe:{pe.shape}")
+            pe = F.interpolate(pe.permute(0, 2, 1), size=x.shape[1], mode="linear", align_corners=False).permute(0, 2, 1)
+        return x + pe[:, :x.size(1)]
+
+
+class CostVolumeDisparityAttention(nn.Module):
+    """Transformer over disparity tokens (core/submodule.py:506-528)."""
+
+    def __init__(self, d_model, nhead, dim_feedforward, dropout=0.1, act=nn.GELU, norm_first=False, num_transformer=6,
+                 max_len=512, resize_embed=False):
+        super().__init__()
+        self.resize_embed = resize_embed
+        self.sa = nn.ModuleList([FlashAttentionTransformerEncoderLayer(embed_dim=d_model, num_heads=nhead,
+                                                                       dim_feedforward=dim_feedforward, act=act,
+                                                                       dropout=dropout)
+                                 for _ in range(num_transformer)])
+        self.pos_embed0 = PositionalEmbedding(d_model, max_len=max_len)
+
+    def forward(self, cv, window_size=(-1, -1)):
+        B, C, D, H, W = cv.shape
+        x = cv.permute(0, 3, 4, 2, 1).reshape(B * H * W, D, C)
+        x = self.pos_embed0(x, resize_embed=self.resize_embed)
+        for layer in self.sa:
+            x = layer(x, window_size=window_size)
+        return x.reshape(B, H, W, D, C).permute(0, 4, 3, 1, 2)
+
+
+class ChannelAttentionEnhancement(nn.Module):
+    """core/submodule.py:532-547."""
+
+    def __init__(self, in_planes, ratio=16):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.max_pool = nn.AdaptiveMaxPool2d(1)
+        self.fc = nn.Sequential(nn.Conv2d(in_planes, in_planes // 16, 1, bias=False), nn.ReLU(),
+                                nn.Conv2d(in_planes // 16, in_planes, 1, bias=False))
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, x):
+        return self.sigmoid(self.fc(self.avg_pool(x)) + self.fc(self.max_pool(x)))
+
+
+class SpatialAttentionExtractor(nn.Module):
+    """core/submodule.py:549-561."""
+
+    def __init__(self, kernel_size=7):
+        super().__init__()
+        self.samconv = nn.Conv2d(2, 1, kernel_size, padding=kernel_size // 2, bias=False)
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, x):
+        t = torch.cat([x.mean(1, keepdim=True), x.amax(1, keepdim=True)], 1)
+        return self.sigmoid(self.samconv(t))
+
+
+class EdgeNextConvEncoder(nn.Module):
+    """Depthwise 7x7 + inverted-bottleneck MLP, residual (core/submodule.py:565-591)."""
+
+    def __init__(self, dim, layer_scale_init_value=1e-6, expan_ratio=4, kernel_size=7, norm="layer"):
+        super().__init__()
+        self.dwconv = nn.Conv2d(dim, dim, kernel_size=kernel_size, padding=kernel_size // 2, groups=dim)
+        self.norm = LayerNorm2d(dim, eps=1e-6) if norm == "layer" else nn.Identity()
+        self.pwconv1 = nn.Linear(dim, expan_ratio * dim)
+        self.act = nn.GELU()
+        self.pwconv2 = nn.Linear(expan_ratio * dim, dim)
+        self.gamma = (nn.Parameter(layer_scale_init_value * torch.ones(dim), requires_grad=True)
+                      if layer_scale_init_value > 0 else None)
+
+    def forward(self, x):
+        y = self.norm(self.dwconv(x)).permute(0, 2, 3, 1)
+        y = self.pwconv2(self.act(self.pwconv1(y)))
+        if self.gamma is not None:
+            y = self.gamma * y
+        return x + y.permute(0, 3, 1, 2)

@@ -1,0 +1,145 @@
+/*
+ * fsmi.h -- C ABI of libfsmi.so, the MI355X-native (gfx950) hot path of
+ * FoundationStereo: cost-volume build, geometry encoding, per-iteration
+ * correlation lookup, soft-argmin, convex upsampling and ConvGRU gates.
+ *
+ * Conventions (every entry point):
+ *   - all tensors are fp32, contiguous, row-major, already resident in device
+ *     memory (HBM); pointers are device pointers, shapes are plain ints;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *     launches are asynchronous on that stream, nothing allocates, nothing
+ *     synchronises, so every call is hipGraph-capturable;
+ *   - return 0 on success, FSMI_ERR_ARG (1001) when an argument violates the
+ *     contract (message in fsmi_last_error()), or the hipError_t of a failed
+ *     launch.
+ *
+ * Reference interfaces replaced are cited as path:line in TongZhe2016/
+ * FoundationStereo (snapshot 2025-06-29).  See INTEGRATION.md for bindings.
+ */
+#ifndef FSMI_H_
+#define FSMI_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSMI_OK 0
+#define FSMI_ERR_ARG 1001
+#define FSMI_MAX_LEVELS 4
+
+/* ---- library ---------------------------------------------------------- */
+int fsmi_version(void);                /* 100*major + minor */
+const char* fsmi_last_error(void);     /* thread-local, "" when none */
+const char* fsmi_arch(void);           /* "gfx950" */
+
+/* ---- a1: group-wise correlation volume --------------------------------
+ * replaces build_gwc_volume / groupwise_correlation, core/submodule.py:388-412
+ * fl, fr: (B,C,H,W); out: (B,G,D,H,W).  out[b,g,d,h,w] = <nL,nR(w-d)> over
+ * the C/G channels of group g after L2 normalisation (eps 1e-12), 0 for w<d.
+ * Requires C % G == 0 (reference: AssertionError at core/submodule.py:390). */
+int fsmi_gwc_volume(const float* fl, const float* fr, float* out,
+                    int B, int C, int G, int D, int H, int W, void* stream);
+
+/* ---- a2: concat volume -------------------------------------------------
+ * replaces build_concat_volume, core/submodule.py:416-427
+ * pl, pr: (B,C,H,W); out: (B,2C,D,H,W): left half copied for all w, right
+ * half shifted by d and zero for w<d. */
+int fsmi_concat_volume(const float* pl, const float* pr, float* out,
+                       int B, int C, int D, int H, int W, void* stream);
+
+/* ---- a1+a2+corr_stem[0] fused ------------------------------------------
+ * replaces core/foundation_stereo.py:207-213 up to and including the
+ * 1x1x1 Conv3d(32 -> Cs) of corr_stem (core/foundation_stereo.py:165):
+ *   out[b,o,d,h,w] = A[b,o,h,w] + [w>=d] Bm[b,o,h,w-d] + sum_g Wg[o,g] gwc[b,g,d,h,w]
+ * where A, Bm: (B,Cs,H,W) are the proj_cmb features already multiplied by the
+ * concat columns of the stem weight (A also carries the stem bias), and
+ * Wg: (Cs,G) the gwc columns.  out: (B,Cs,D,H,W). */
+int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, const float* Bm,
+                          const float* Wg, float* out,
+                          int B, int C, int G, int Cs, int D, int H, int W, void* stream);
+
+/* pointwise 2-output projection used to form A / Bm above:
+ * out[b,o,h,w] = bias[o] + sum_c Wt[o,c] x[b,c,h,w];  x: (B,C,H,W), out: (B,O,H,W) */
+int fsmi_pointwise_proj(const float* x, const float* Wt, const float* bias, float* out,
+                        int B, int C, int O, int H, int W, void* stream);
+
+/* ---- a5: all-pairs correlation + W2 pyramid (fp32 MFMA) ----------------
+ * replaces Combined_Geo_Encoding_Volume.corr + its avg-pool pyramid,
+ * core/geometry.py:24-40,68-77.  fl, fr: (B,C,H,W).  levels[i]: (B,H,W,W>>i')
+ * with W_i = floor(W_{i-1}/2); level 0 is the full (B,H,W1,W2) correlation of
+ * the channel-L2-normalised features. */
+int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, int num_levels,
+                       int B, int C, int H, int W, void* stream);
+
+/* ---- a5: filtered-volume pyramid over D ---------------------------------
+ * replaces core/geometry.py:29,34-36 without the permute copy.  vol:
+ * (B,Cv,D,H,W) native layout; levels[i-1]: (B,Cv,D_i,H,W), i=1..num_levels-1,
+ * D_i = floor(D_{i-1}/2), value = mean of the two parents (iterated). */
+int fsmi_volume_pyramid(const float* vol, float* const* levels, int num_levels,
+                        int B, int Cv, int D, int H, int W, void* stream);
+
+/* ---- a6: per-iteration multi-level lookup ------------------------------
+ * replaces Combined_Geo_Encoding_Volume.__call__ + bilinear_sampler,
+ * core/geometry.py:43-65, core/utils/utils.py:44-55.
+ * vol_levels[i]: (B,Cv,D_i,H,W); corr_levels[i]: (B,H,W,W2_i); disp: (B,1,H,W);
+ * out: (B, L*(2r+1)*(Cv+1), H, W) with channel order per level
+ * [geo (c*(2r+1)+k) ..., corr k ...] (core/geometry.py:62-65).
+ * Taps at x = disp/2^i + k and x = w/2^i - disp/2^i + k, k in [-r,r]; linear
+ * interpolation, align_corners=True, zero padding.  Requires D_i >= 2, W2_i >= 2. */
+int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_levels,
+                    const float* disp, float* out,
+                    int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
+                    void* stream);
+
+/* 1-D stereo specialisation of bilinear_sampler (core/utils/utils.py:44-55):
+ * img (P,C,1,Lx); x (P,K) pixel x-coordinates (y == 0); out (P,C,1,K). */
+int fsmi_bilinear_sampler_1d(const float* img, const float* x, float* out,
+                             int P, int C, int Lx, int K, void* stream);
+
+/* ---- a4: soft-argmin ---------------------------------------------------
+ * fsmi_disparity_regression: core/submodule.py:431-435, prob (B,D,H,W) -> (B,1,H,W)
+ * fsmi_softmax_regression:  core/foundation_stereo.py:218-220 fused
+ *                           (softmax over D of logits, then sum d*p_d). */
+int fsmi_disparity_regression(const float* prob, float* out, int B, int D, int H, int W, void* stream);
+int fsmi_softmax_regression(const float* logits, float* out, int B, int D, int H, int W, void* stream);
+
+/* ---- a9: convex upsampling ---------------------------------------------
+ * fsmi_context_upsample: core/submodule.py:456-468; disp (B,1,h,w),
+ *   w (B,9,4h,4w) -> out (B,4h,4w).
+ * fsmi_softmax_context_upsample: core/foundation_stereo.py:187-189 fused:
+ *   softmax over the 9 logits, scale disp by `scale` (4.0), convex combine. */
+int fsmi_context_upsample(const float* disp, const float* w, float* out, int B, int h, int w_, void* stream);
+int fsmi_softmax_context_upsample(const float* disp, const float* logits, float* out, float scale,
+                                  int B, int h, int w_, void* stream);
+
+/* ---- a7: selective ConvGRU gates (core/update.py:83-119) ----------------
+ * zr_s / zr_l: (B, 2*Hd, H, W) pre-activations [z | r] of the small (k=1) and
+ * large (k=3) RaftConvGRU; h: (B,Hd,H,W); x: (B,Cx,H,W).
+ * fsmi_gru_reset: qin_s/qin_l (B, Hd+Cx, H, W) <- [sigmoid(r)*h , x]   (update.py:92-93)
+ * fsmi_gru_blend: hout <- att*((1-zs)h+zs*tanh(qs)) + (1-att)*((1-zl)h+zl*tanh(ql))
+ *                 with z = sigmoid(z_pre); q_s/q_l: (B,Hd,H,W); att (B,1,H,W);
+ *                 (update.py:91,94-95,117). hout may alias h. */
+int fsmi_gru_reset(const float* zr_s, const float* zr_l, const float* h, const float* x,
+                   float* qin_s, float* qin_l, int B, int Hd, int Cx, int H, int W, void* stream);
+int fsmi_gru_blend(const float* zr_s, const float* zr_l, const float* q_s, const float* q_l,
+                   const float* h, const float* att, float* hout,
+                   int B, int Hd, int H, int W, void* stream);
+
+/* ---- live kernel timing (bench.py roofline) -----------------------------
+ * When enabled, every launch of the kernels below is bracketed by a pair of
+ * hipEvents recorded on the launch stream (skipped while the stream is being
+ * captured).  fsmi_timer_query synchronises those events and returns the
+ * summed duration and launch count since the last reset. */
+enum {
+  FSMI_K_GWC = 0, FSMI_K_CONCAT, FSMI_K_COMB, FSMI_K_PROJ, FSMI_K_CORR, FSMI_K_VOLPYR,
+  FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
+  FSMI_K_COUNT
+};
+int fsmi_timer_enable(int on);
+int fsmi_timer_reset(void);
+int fsmi_timer_query(int kernel, double* total_ms, long long* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSMI_H_ */

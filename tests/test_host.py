@@ -1,0 +1,102 @@
+"""CPU-only checks of the host side: module-tree / state_dict compatibility,
+the C-ABI library's exported surface, host logic and loud failure on CPU."""
+import re
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from foundationstereo_amd import synth
+from tests.helpers import reference_keys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("vit", ["vits", "vitl"])
+def test_state_dict_matches_reference(vit):
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    args = synth.make_args(max_disp=192, corr_levels=4, vit_size=vit)
+    mine = {k: tuple(v.shape) for k, v in FoundationStereo(args).state_dict().items()}
+    ref = dict(reference_keys(vit))
+    assert set(mine) == set(ref), (sorted(set(mine) - set(ref))[:10], sorted(set(ref) - set(mine))[:10])
+    for k in ref:
+        assert mine[k] == ref[k], k
+
+
+def test_state_dict_order_matches_reference():
+    """Key order matters where the reference shares a module under two names (norm3 / downsample.1)."""
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    args = synth.make_args(max_disp=192, corr_levels=4, vit_size="vits")
+    mine = list(FoundationStereo(args).state_dict().keys())
+    ref = [k for k, _ in reference_keys("vits")]
+    assert mine == ref
+
+
+def _header_symbols():
+    txt = open(os.path.join(REPO, "include", "fsmi.h")).read()
+    return sorted(set(re.findall(r"\b(fsmi_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    from foundationstereo_amd import _lib
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+    assert lib.fsmi_arch() == b"gfx950"
+    assert lib.fsmi_version() >= 100
+
+
+def test_library_rejects_bad_args_without_gpu():
+    """Argument validation happens before any HIP call, so it is testable on the CPU."""
+    from foundationstereo_amd import _lib
+    lib = _lib.load()
+    rc = lib.fsmi_gwc_volume(1, 1, 1, 1, 30, 8, 4, 2, 8, None)
+    assert rc == 1001 and b"num_groups" in lib.fsmi_last_error()
+    rc = lib.fsmi_geo_lookup(None, None, None, None, 2, 4, 1, 28, 8, 2, 8, 8, None)
+    assert rc == 1001
+
+
+def test_ops_refuse_cpu_tensors():
+    from foundationstereo_amd import ops
+    x = torch.zeros(1, 16, 2, 8)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        ops.gwc_volume(x, x, 4, 8)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        ops.softmax_regression(torch.zeros(1, 4, 2, 2))
+
+
+def test_gwc_assertion_mirrors_reference():
+    from foundationstereo_amd import submodule
+    x = torch.zeros(1, 30, 2, 8)
+    with pytest.raises((AssertionError, RuntimeError)):
+        submodule.build_gwc_volume(x, x, 4, 8)
+
+
+@pytest.mark.parametrize("hw", [(240, 320), (375, 1242), (256, 320), (1, 31)])
+def test_input_padder(hw):
+    from foundationstereo_amd.utils import InputPadder
+    x = torch.arange(hw[0] * hw[1], dtype=torch.float32).reshape(1, 1, *hw)
+    p = InputPadder(x.shape, divis_by=32)
+    (y,) = p.pad(x)
+    assert y.shape[-2] % 32 == 0 and y.shape[-1] % 32 == 0
+    assert torch.equal(p.unpad(y), x)
+    pad_ht = (((hw[0] // 32) + 1) * 32 - hw[0]) % 32   # core/utils/utils.py:26
+    pad_wd = (((hw[1] // 32) + 1) * 32 - hw[1]) % 32
+    assert p._pad == [pad_wd // 2, pad_wd - pad_wd // 2, pad_ht // 2, pad_ht - pad_ht // 2]
+
+
+def test_args_access_modes():
+    a = synth.make_args(max_disp=64)
+    assert a.max_disp == a["max_disp"] == a.get("max_disp") == 64
+    assert a.get("low_memory") is False
+
+
+def test_synth_is_deterministic():
+    a = synth.normal(synth.name_seed("x"), (4, 5))
+    b = synth.normal(synth.name_seed("x"), (4, 5))
+    assert np.array_equal(a, b)
+    assert abs(float(synth.normal(7, (100000,)).std()) - 1.0) < 0.02
