@@ -236,6 +236,11 @@ int fsmi_gwc_volume(const float* fl, const float* fr, float* out, int B, int C, 
   const int nDC = (D + DC - 1) / DC;
   const unsigned grid = static_cast<unsigned>(B) * H * nDC;
   hipStream_t s = as_stream(stream);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gwc_kernel<kNout>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return finish_launch("fsmi_gwc_volume: LDS attribute");
+  }
   LaunchTimer t(FSMI_K_GWC, s);
   hipLaunchKernelGGL(gwc_kernel<kNout>, dim3(grid), dim3(kThreads), lds, s, fl, fr, out, C, G, D, H, W, DC, nDC);
   return finish_launch("fsmi_gwc_volume");
@@ -266,6 +271,11 @@ int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, cons
   const int nDC = (D + DC - 1) / DC;
   const unsigned grid = static_cast<unsigned>(B) * H * nDC;
   hipStream_t s = as_stream(stream);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(comb_stem_kernel<8, kNout>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return finish_launch("fsmi_comb_volume_stem: LDS attribute");
+  }
   LaunchTimer t(FSMI_K_COMB, s);
   hipLaunchKernelGGL((comb_stem_kernel<8, kNout>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs,
                      D, H, W, DC, nDC);

@@ -164,7 +164,12 @@ struct LookupArgs {
   int L, Cv, D, H, W, W2, B;
 };
 
+// FP contraction is OFF for the coordinate math: fusing `ix - floor(ix)` into
+// fma(h, x'+1, -floor) computes the fraction from the UNROUNDED ix and moves
+// samples near integer positions by up to an ulp of ix (seen as 1e-5 errors
+// at x ~ 80 on gfx950 before this pragma).
 __device__ __forceinline__ float unnorm(float x, int n) {
+#pragma clang fp contract(off)
   const float xn = (2.f * x) / static_cast<float>(n - 1) - 1.f;
   return (xn + 1.f) * (static_cast<float>(n - 1) / 2.f);
 }
@@ -172,6 +177,7 @@ __device__ __forceinline__ float unnorm(float x, int n) {
 template <int R>
 __device__ __forceinline__ void sample_taps(const float* __restrict__ src, size_t stride, int n, float xc,
                                             float* __restrict__ dst, size_t dstride) {
+#pragma clang fp contract(off)
   constexpr int K = 2 * R + 1, NW = 2 * R + 4;
   // xc = centre coordinate (tap k sits at xc + (k - R)); clamp keeps int math defined
   const float xcl = fminf(fmaxf(xc, -1.0e6f), 1.0e6f);
@@ -232,6 +238,7 @@ __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
 __global__ __launch_bounds__(256) void sampler_kernel(const float* __restrict__ img, const float* __restrict__ xs,
                                                       float* __restrict__ out, int C, int Lx, int K,
                                                       long long total) {
+#pragma clang fp contract(off)
   const long long idx = blockIdx.x * 256ll + threadIdx.x;
   if (idx >= total) return;
   const int k = static_cast<int>(idx % K);

@@ -36,7 +36,10 @@ def _check(name: str, *ts: Tensor):
 
 
 def _c(t: Tensor) -> Tensor:
-    return t if t.is_contiguous() else t.contiguous()
+    """Contiguous and 16-byte aligned (the kernels issue float4 accesses)."""
+    if t.is_contiguous() and t.data_ptr() % 16 == 0:
+        return t
+    return t.contiguous() if not t.is_contiguous() else t.clone()
 
 
 def _p(t: Tensor) -> int:

@@ -1,0 +1,270 @@
+"""GPU parity: the HIP hot path (through the C ABI) vs the CPU oracle and the reference goldens.
+
+Tolerances (fp32 everywhere; the north-star bar is |dd| < 1e-3 px end to end):
+* per-op kernels vs oracle / golden: abs 1e-5 (different fp32 summation order only);
+* all-pairs correlation (K = C products, normalised operands): abs 2e-6 + 2e-6*|x|;
+* end-to-end disparity vs oracle and vs the reference golden: max |dd| < 1e-3 px.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from foundationstereo_amd import synth
+from tests.helpers import load_golden, model_keys, oracle_params, t
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def g(a):
+    return t(a).to(DEV)
+
+
+@pytest.fixture(scope="module")
+def ops_mod():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from foundationstereo_amd import _lib, ops
+    _lib.load()
+    return ops
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return load_golden("ops_small")
+
+
+def close(a, b, atol=1e-5, rtol=0.0):
+    a = a.detach().float().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    b = b.detach().float().cpu().numpy() if isinstance(b, torch.Tensor) else b
+    np.testing.assert_allclose(a, b, atol=atol, rtol=rtol)
+
+
+# ------------------------------------------------------------------ a1 / a2
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_gwc_golden(ops_mod, gold, tag):
+    B, C, G, H, W, D = (int(v) for v in gold[f"gwc_{tag}_meta"])
+    out = ops_mod.gwc_volume(g(gold[f"gwc_{tag}_fl"]), g(gold[f"gwc_{tag}_fr"]), D, G)
+    close(out, gold[f"gwc_{tag}_out"])
+    assert torch.all(out[:, :, 1:, :, 0] == 0)
+
+
+@pytest.mark.parametrize("shape", [(1, 128, 8, 5, 40, 48), (2, 224, 8, 3, 24, 30), (1, 32, 8, 2, 11, 7)])
+def test_gwc_vs_oracle(ops_mod, shape):
+    B, C, G, H, W, D = shape
+    fl = synth.normal(11, (B, C, H, W))
+    fr = synth.normal(12, (B, C, H, W))
+    close(ops_mod.gwc_volume(g(fl), g(fr), D, G), oracle.build_gwc_volume(t(fl), t(fr), D, G))
+
+
+def test_concat_golden(ops_mod, gold):
+    B, C, H, W, D = (int(v) for v in gold["concat_meta"])
+    out = ops_mod.concat_volume(g(gold["concat_pl"]), g(gold["concat_pr"]), D)
+    assert np.array_equal(out.cpu().numpy(), gold["concat_out"])
+
+
+@pytest.mark.parametrize("vit,W", [("vits", 40), ("vitl", 24), ("vits", 13)])
+def test_comb_volume_stem_vs_oracle(ops_mod, vit, W):
+    """Fused gwc+concat+corr_stem[0] == Conv3d_1x1(cat(gwc, concat(proj(fl), proj(fr))))."""
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    args = synth.make_args(max_disp=64, corr_levels=2, vit_size=vit)
+    m = FoundationStereo(args)
+    synth.init_module_(m, seed=5)
+    m = m.to(DEV).eval()
+    C = m.feature.d_out[0]
+    B, H, D = 2, 3, 16
+    fl, fr = synth.normal(21, (B, C, H, W)), synth.normal(22, (B, C, H, W))
+    args["max_disp"] = 4 * D
+    with torch.no_grad():
+        out = m.build_stem_volume(g(fl), g(fr))
+        P = {k: v.cpu() for k, v in m.state_dict().items()}
+        comb = torch.cat([oracle.build_gwc_volume(t(fl), t(fr), D, 8),
+                          oracle.build_concat_volume(oracle.stereo_oracle._conv(P, "proj_cmb", t(fl)),
+                                                     oracle.stereo_oracle._conv(P, "proj_cmb", t(fr)), D)], 1)
+        ref = oracle.stereo_oracle._conv(P, "corr_stem.0", comb)
+        m.fused_volume = False
+        unfused = m.build_stem_volume(g(fl), g(fr))
+    close(out, ref, atol=2e-5)
+    close(unfused, ref, atol=2e-5)
+
+
+# ------------------------------------------------------------------ a4 / a9
+
+def test_regression_golden(ops_mod, gold):
+    close(ops_mod.disparity_regression(g(gold["reg_prob"]), 16), gold["reg_out"])
+    close(ops_mod.softmax_regression(g(gold["reg_logits"])), gold["reg_out"], atol=2e-5)
+
+
+def test_upsample_golden(ops_mod, gold):
+    close(ops_mod.context_upsample(g(gold["up_disp"]), g(gold["up_w"])), gold["up_out"])
+
+
+def test_softmax_upsample_vs_oracle(ops_mod):
+    d = synth.normal(31, (2, 1, 6, 10), 7.0)
+    lg = synth.normal(32, (2, 9, 24, 40), 2.0)
+    ref = oracle.context_upsample(t(d) * 4.0, torch.softmax(t(lg), 1))
+    close(ops_mod.softmax_context_upsample(g(d), g(lg), 4.0), ref, atol=2e-5)
+
+
+# ------------------------------------------------------------------ a5 / a6
+
+@pytest.mark.parametrize("L", [2, 4])
+def test_geo_encoding_golden(ops_mod, gold, L):
+    from foundationstereo_amd.geometry import Combined_Geo_Encoding_Volume
+    p = f"geo{L}_"
+    dx = torch.linspace(-4, 4, 9).reshape(1, 1, 9, 1)
+    ge = Combined_Geo_Encoding_Volume(g(gold[p + "f1"]), g(gold[p + "f2"]), g(gold[p + "vol"]), num_levels=L, dx=dx)
+    for i in range(L):
+        close(ge.init_corr_pyramid[i].reshape(-1), gold[p + f"corrpyr{i}"].reshape(-1), atol=4e-6)
+    close(ge.geo_volume_pyramid[1].permute(0, 3, 4, 1, 2).reshape(-1), gold[p + "volpyr1"].reshape(-1), atol=1e-6)
+    out = ge(g(gold[p + "disp"]))
+    close(out, gold[p + "out"], atol=1e-5)
+
+
+@pytest.mark.parametrize("C,H,W", [(128, 3, 160), (224, 2, 96), (32, 2, 24), (64, 1, 70)])
+def test_allpairs_corr_vs_oracle(ops_mod, C, H, W):
+    f1, f2 = synth.normal(41, (2, C, H, W)), synth.normal(42, (2, C, H, W))
+    lv = ops_mod.allpairs_corr(g(f1), g(f2), 4)
+    ref = oracle.allpairs_corr(t(f1), t(f2))
+    for i in range(4):
+        close(lv[i], ref, atol=3e-6)
+        ref = oracle.stereo_oracle._pool_last(ref)
+
+
+@pytest.mark.parametrize("D,L", [(48, 4), (20, 4), (17, 2), (80, 3)])
+def test_volume_pyramid_vs_oracle(ops_mod, D, L):
+    v = synth.normal(51, (2, 5, D, 3, 20))
+    lv = ops_mod.volume_pyramid(g(v), L)
+    ref = t(v).permute(0, 1, 3, 4, 2)
+    for i in range(1, L):
+        ref = oracle.stereo_oracle._pool_last(ref)
+        assert torch.equal(lv[i].cpu(), ref.permute(0, 1, 4, 2, 3).contiguous())
+
+
+@pytest.mark.parametrize("L,D,W", [(2, 48, 160), (4, 48, 160), (4, 80, 96), (2, 16, 40)])
+def test_lookup_vs_oracle(ops_mod, L, D, W):
+    """Includes disparities below 0, beyond D and exact integers (border / floor cases)."""
+    from foundationstereo_amd.geometry import Combined_Geo_Encoding_Volume
+    B, C, Cv, H = 1, 64, 28, 4
+    f1, f2 = synth.normal(61, (B, C, H, W)), synth.normal(62, (B, C, H, W))
+    vol = synth.normal(63, (B, Cv, D, H, W))
+    disp = synth.uniform(64, (B, 1, H, W), -8.0, D + 8.0)
+    disp[0, 0, 0, :6] = [0.0, 1.0, D - 1.0, D, -1.0, 2.5]
+    ge = Combined_Geo_Encoding_Volume(g(f1), g(f2), g(vol), num_levels=L, dx=torch.linspace(-4, 4, 9))
+    out = ge(g(disp))
+    ref = oracle.GeoEncoding(t(f1), t(f2), t(vol), L, 4)
+    coords = torch.arange(W, dtype=torch.float).view(1, 1, W, 1).repeat(B, H, 1, 1)
+    close(out, ref(t(disp), coords), atol=1e-5)
+
+
+def test_bilinear_sampler_golden(ops_mod, gold):
+    from foundationstereo_amd.utils import bilinear_sampler
+    close(bilinear_sampler(g(gold["bs_img"]), g(gold["bs_coords"])), gold["bs_out"])
+
+
+# ------------------------------------------------------------------ a7
+
+def test_gru_gates_vs_torch(ops_mod):
+    B, Hd, Cx, H, W = 2, 16, 24, 5, 7
+    zr_s, zr_l = (g(synth.normal(s, (B, 2 * Hd, H, W), 2.0)) for s in (71, 72))
+    h, x = g(synth.normal(73, (B, Hd, H, W))), g(synth.normal(74, (B, Cx, H, W)))
+    qs_in, ql_in = ops_mod.gru_reset(zr_s, zr_l, h, x)
+    close(qs_in, torch.cat([torch.sigmoid(zr_s[:, Hd:]) * h, x], 1), atol=1e-6)
+    close(ql_in, torch.cat([torch.sigmoid(zr_l[:, Hd:]) * h, x], 1), atol=1e-6)
+    q_s, q_l = (g(synth.normal(s, (B, Hd, H, W), 2.0)) for s in (75, 76))
+    att = g(synth.uniform(77, (B, 1, H, W)))
+    out = ops_mod.gru_blend(zr_s, zr_l, q_s, q_l, h, att)
+    zs, zl = torch.sigmoid(zr_s[:, :Hd]), torch.sigmoid(zr_l[:, :Hd])
+    ref = ((1 - zs) * h + zs * torch.tanh(q_s)) * att + ((1 - zl) * h + zl * torch.tanh(q_l)) * (1 - att)
+    close(out, ref, atol=1e-6)
+
+
+def test_update_step_golden(ops_mod):
+    gd = load_golden("update_step")
+    from foundationstereo_amd.update import BasicSelectiveMultiUpdateBlock
+    args = synth.make_args(max_disp=64, corr_levels=2)
+    blk = BasicSelectiveMultiUpdateBlock(args, 128, volume_dim=28)
+    synth.init_module_(blk, seed=77)
+    blk = blk.to(DEV).eval()
+    with torch.no_grad():
+        net, mask, delta = blk([g(gd[f"net{i}"]) for i in range(3)], [g(gd[f"inp{i}"]) for i in range(3)],
+                               g(gd["corr"]), g(gd["disp"]), [g(gd[f"att{i}"]) for i in range(3)])
+    for i in range(3):
+        close(net[i], gd[f"onet{i}"], atol=5e-5)
+    close(mask, gd["mask"], atol=5e-5)
+    close(delta, gd["delta"], atol=5e-5)
+
+
+# ------------------------------------------------------------------ end to end
+
+def _product(args, H, W, shift, seed=1234):
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    m = FoundationStereo(args).eval()
+    synth.init_module_(m, seed=seed)
+    m = m.to(DEV)
+    fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, shift_px=shift)
+    m.feature.set_features([g(a) for a in fl], [g(a) for a in fr], g(vf))
+    left, right = synth.stereo_images(1, H, W)
+    return m, (fl, fr, vf), (left, right)
+
+
+@pytest.mark.parametrize("name", ["e2e_tiny", "e2e_cfg1_L2", "e2e_cfg1_L4"])
+def test_e2e_vs_reference_golden(ops_mod, name):
+    gd = load_golden(name)
+    H, W, md, iters, L, shift = (int(v) for v in gd["meta"])
+    args = synth.make_args(max_disp=md, corr_levels=L, vit_size="vits")
+    m, _, (left, right) = _product(args, H, W, shift)
+    with torch.no_grad():
+        out = m(g(left), g(right), iters=iters, test_mode=True)
+    d = float(np.abs(out.cpu().numpy() - gd["disp"]).max())
+    assert d < 1e-3, f"max |dd| vs reference = {d} px"
+
+
+@pytest.mark.parametrize("H,W,md,iters,L,vit", [(480, 640, 192, 2, 4, "vits"), (256, 320, 64, 4, 2, "vitl")])
+def test_e2e_vs_oracle(ops_mod, H, W, md, iters, L, vit):
+    """cfg2 geometry (640x480, D192, L=4) at reduced iterations; the oracle runs on the host CPU."""
+    args = synth.make_args(max_disp=md, corr_levels=L, vit_size=vit)
+    m, (fl, fr, vf), (left, right) = _product(args, H, W, 8)
+    with torch.no_grad():
+        out = m(g(left), g(right), iters=iters, test_mode=True).cpu()
+        P = {k: v.cpu() for k, v in m.state_dict().items()}
+        ref = oracle.oracle_forward(P, args, t(left), t(right), [t(a) for a in fl], [t(a) for a in fr], t(vf),
+                                    iters=iters)
+    d = float((out - ref).abs().max())
+    assert d < 1e-3, f"max |dd| vs oracle = {d} px"
+
+
+def test_batch_invariance(ops_mod):
+    """Pairs are independent: B=2 == two B=1 runs (the basis of batch sharding)."""
+    args = synth.make_args(max_disp=32, corr_levels=2, vit_size="vits")
+    H, W = 64, 96
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    m = FoundationStereo(args).eval()
+    synth.init_module_(m, seed=3)
+    m = m.to(DEV)
+    fl, fr, vf = synth.backbone_features(2, H, W, "vits", shift_px=2)
+    left, right = synth.stereo_images(2, H, W)
+    with torch.no_grad():
+        m.feature.set_features([g(a) for a in fl], [g(a) for a in fr], g(vf))
+        both = m(g(left), g(right), iters=3, test_mode=True)
+        singles = []
+        for i in range(2):
+            m.feature.set_features([g(a[i:i + 1]) for a in fl], [g(a[i:i + 1]) for a in fr], g(vf[i:i + 1]))
+            singles.append(m(g(left[i:i + 1]), g(right[i:i + 1]), iters=3, test_mode=True))
+    close(both, torch.cat(singles, 0), atol=1e-4)
+
+
+def test_hierarchical_runs(ops_mod):
+    """cfg5 driver (run_hierachical) end to end at a small size, vs the oracle's two-pass restatement."""
+    args = synth.make_args(max_disp=64, corr_levels=2, vit_size="vits")
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    m = FoundationStereo(args).eval()
+    synth.init_module_(m, seed=9)
+    m = m.to(DEV)
+    left, right = synth.stereo_images(1, 200, 300)
+    with torch.no_grad():
+        out = m.run_hierachical(g(left), g(right), iters=2, test_mode=True)
+    assert out.shape == (1, 1, 200, 300) and torch.isfinite(out).all()
