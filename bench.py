@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Throughput of the FoundationStereo hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+
+A step = one ``FoundationStereo.forward(test_mode=True)`` over this rank's
+pairs: cost-volume build, 3D filtering, context net, geometry encoding, 32
+refinement iterations (lookup + ConvGRU update), convex upsampling.  Inputs
+(images and the synthetic backbone's feature maps) are resident
+in HBM before the timed region; the out-of-scope backbone is not run.
+Multi-GPU: the image batch is broadcast from rank 0 every step and the
+disparities all-gathered back (RCCL over xGMI), weights broadcast once.
+
+Rank 0 prints ONE JSON line.  ``roofline`` is the dominant HBM-bound kernel
+(the per-iteration geometry lookup), timed with HIP events on its launch
+stream over the timed region; ``cpu_baseline`` is the CPU oracle run on the
+host cores for one pair of the same workload (N=1, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from foundationstereo_amd import dist as fdist  # noqa: E402
+from foundationstereo_amd import synth  # noqa: E402
+
+HBM_PEAK = 8.0e12  # MI355X HBM3E spec, B/s (MI355X_MICROARCH.md chip table)
+
+# BASELINE.json configs (name -> H, W, max_disp, iters, vit, pairs per GPU)
+CONFIGS = {
+    "cfg1": (256, 320, 64, 8, "vits", 1),     # 320x240 padded to /32
+    "cfg2": (480, 640, 192, 32, "vits", 1),
+    "cfg3": (480, 640, 192, 32, "vitl", 4),   # batch 32 over 8 GPUs
+    "cfg4": (384, 1248, 256, 32, "vitl", 1),  # batch 8 over 8 GPUs
+    "tiny": (64, 96, 32, 4, "vits", 1),
+}
+
+
+def lookup_bytes(B, H4, W4, Cv, L, r):
+    """Algorithmic HBM bytes of one lookup launch: read disp, read
+    the 2r+2 touched taps of Cv+1 channels per level, write 2r+1 of them."""
+    K = 2 * r + 1
+    N = H4 * W4
+    return 4 * B * N * (1 + L * (Cv + 1) * (K + 1) + L * K * (Cv + 1))
+
+
+def build_bytes(B, C, H4, W4, D4, Cs=28):
+    """Algorithmic bytes of the fused comb-volume+stem kernel: read fl, fr, A, Bm; write (B,Cs,D4,H4,W4)."""
+    N = H4 * W4
+    return 4 * B * N * (2 * C + 2 * Cs + Cs * D4)
+
+
+def make_model(args, device, rank):
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    m = FoundationStereo(args).eval()
+    if rank == 0:
+        synth.init_module_(m, seed=1234)
+    m = m.to(device)
+    fdist.broadcast_module_(m, src=0)
+    return m
+
+
+def cpu_baseline(args, H, W, iters, threads):
+    """Time the CPU oracle on one pair of the same workload on the host cores."""
+    import oracle
+    torch.set_num_threads(threads)
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    m = FoundationStereo(args)
+    synth.init_module_(m, seed=1234)
+    P = {k: v.float() if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, shift_px=8)
+    left, right = synth.stereo_images(1, H, W)
+    T = oracle.StageTimer()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
+                              [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr],
+                              torch.from_numpy(vf), iters=iters, timer=T)
+    dt = time.perf_counter() - t0
+    return dt, T.stages
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--corr-levels", type=int, default=4)
+    ap.add_argument("--pairs-per-gpu", type=int, default=0, help="override the config's pairs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mixed-precision", action="store_true",
+                    help="fp16 autocast for the dense convs (the reference GPU default); volumes/lookup stay fp32")
+    a = ap.parse_args()
+
+    rank, local, world = fdist.init_from_env("nccl")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    torch.backends.cudnn.benchmark = True
+    H, W, md, iters, vit, per_gpu = CONFIGS[a.config]
+    if a.pairs_per_gpu:
+        per_gpu = a.pairs_per_gpu
+    L = a.corr_levels
+    args = synth.make_args(max_disp=md, corr_levels=L, vit_size=vit, mixed_precision=a.mixed_precision)
+    model = make_model(args, device, rank)
+
+    from foundationstereo_amd import _lib, ops
+    _lib.load()
+    B = per_gpu * world
+    lo, hi = fdist.shard_range(B, rank, world)
+    # this rank's backbone output, resident in HBM (seed = 0x5EED + global pair index)
+    feats = [synth.backbone_features(1, H, W, vit, seed=0x5EED + i, shift_px=8) for i in range(lo, hi)]
+    fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(device) for j in range(4)]
+    fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(device) for j in range(4)]
+    vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(device)
+    model.feature.set_features(fl, fr, vf)
+    if rank == 0:
+        left, right = synth.stereo_images(B, H, W)
+        batch = torch.from_numpy(np.stack([left, right], 1)).to(device)
+    else:
+        batch = torch.empty((B, 2, 3, H, W), device=device)
+
+    def fn(lft, rgt):
+        return model(lft, rgt, iters=iters, test_mode=True)
+
+    runner = fdist.ShardedStereo(fn, rank, world)
+
+    def step():
+        with torch.no_grad():
+            return runner.step(batch, (1, H, W))
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    ops.timer_enable(True)
+    ops.timer_reset()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lk_ms, lk_n = ops.timer_query("lookup")
+    cb_ms, cb_n = ops.timer_query("comb")
+    ops.timer_enable(False)
+    assert torch.isfinite(out).all()
+
+    H4, W4, D4 = H // 4, W // 4, md // 4
+    bl = hi - lo
+    lk_bytes = lookup_bytes(bl, H4, W4, 28, L, args.corr_radius)
+    lk_avg = (lk_ms / 1e3) / max(lk_n, 1)
+    C = synth.feature_dims(vit)[0][0]
+    cb_bytes = build_bytes(bl, C, H4, W4, D4)
+    cb_avg = (cb_ms / 1e3) / max(cb_n, 1)
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_lookup_summary.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        if pmc.get("config") == a.config and pmc.get("corr_levels") == L:
+            traffic = pmc.get("hbm_bytes_per_launch")
+
+    pairs = a.steps * B
+    res = {
+        "metric": "stereo pairs/sec (32 refinement iters)",
+        "value": pairs / elapsed,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * elapsed / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16-conv/f32-volume" if a.mixed_precision else "f32",
+        "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
+        "config": {"workload": f"{a.config}: {W}x{H}, max_disp {md}, {iters} iters, {vit}, "
+                               f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",
+                   "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,
+                   "corr_levels": L, "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "geo_lookup", "bound": "hbm", "achieved": lk_bytes / lk_avg / 1e9,
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
+                     "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,
+                     "launches": lk_n},
+        "roofline_build": {"kernel": "comb_volume_stem", "bound": "hbm",
+                           "achieved": cb_bytes / cb_avg / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
+                           "unit": "GB/s", "frac": cb_bytes / cb_avg / HBM_PEAK if cb_n else None,
+                           "algorithmic_bytes": cb_bytes, "avg_us": cb_avg * 1e6, "launches": cb_n},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(os.cpu_count() or 1, 16)
+        dt, stages = cpu_baseline(args, H, W, iters, threads)
+        res["cpu_baseline"] = {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+                               "sample": f"1 pair of {a.config} (all {iters} iterations) through the fp32 "
+                                         f"torch-CPU oracle, {dt:.1f} s",
+                               "stages_s": {k: round(v, 3) for k, v in stages.items()}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
