@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--corr-levels", type=int, default=4)
     ap.add_argument("--pairs-per-gpu", type=int, default=0, help="override the config's pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("FSMI_CUDNN_BENCHMARK", "0")),
+                    help="MIOpen Find (exhaustive, slow first call) instead of immediate-mode heuristics")
     ap.add_argument("--mixed-precision", action="store_true",
                     help="fp16 autocast for the dense convs (the reference GPU default); volumes/lookup stay fp32")
     a = ap.parse_args()
@@ -107,7 +109,8 @@ def main():
     rank, local, world = fdist.init_from_env("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = bool(a.cudnn_benchmark)
+    t_setup = time.perf_counter()
     H, W, md, iters, vit, per_gpu = CONFIGS[a.config]
     if a.pairs_per_gpu:
         per_gpu = a.pairs_per_gpu
@@ -140,9 +143,12 @@ def main():
         with torch.no_grad():
             return runner.step(batch, (1, H, W))
 
+    t_warm = time.perf_counter()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    if rank == 0:
+        print(f"[bench] setup {t_warm - t_setup:.1f}s warmup {time.perf_counter() - t_warm:.1f}s", file=sys.stderr)
     ops.timer_enable(True)
     ops.timer_reset()
     if world > 1:

@@ -5,7 +5,19 @@ loaded via ctypes from ``_lib/libfsmi.so``) behind the reference's own module
 and function API (``submodule``, ``geometry``, ``update``, ``utils``,
 ``foundation_stereo``).  See DESIGN.md.
 """
+import os as _os
+
 __version__ = "0.1.0"
+
+# MIOpen runs the dense convolutions.  Its exhaustive Find benchmarks naive
+# kernels (seconds each for the 3D deconvs) on first use; instead ship the
+# find-db measured on MI355X for these layer shapes (tuning/miopen) and use
+# FAST mode: db hit -> tuned solver, miss -> immediate-mode heuristic, never a
+# search.  Both are only defaults; an explicit environment wins.
+_TUNING = _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))), "tuning", "miopen")
+_os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+if _os.path.isdir(_TUNING):
+    _os.environ.setdefault("MIOPEN_USER_DB_PATH", _TUNING)
 
 
 def patch_reference(core_foundation_stereo_module):

@@ -137,12 +137,14 @@ class SelectiveConvGRU(nn.Module):
         x = torch.cat(x, dim=1) if len(x) > 1 else x[0]
         x = self.conv0(x)
         hx = self.conv1(torch.cat([x, h], dim=1))
-        zr_s = self.small_gru.zr(hx)
-        zr_l = self.large_gru.zr(hx)
-        qs_in, ql_in = ops.gru_reset(zr_s, zr_l, h, x)
-        q_s = self.small_gru.convq(qs_in)
-        q_l = self.large_gru.convq(ql_in)
-        return ops.gru_blend(zr_s, zr_l, q_s, q_l, h, att)
+        # .float(): no-ops in fp32; under the reference's fp16 autocast the gates stay fp32
+        zr_s = self.small_gru.zr(hx).float()
+        zr_l = self.large_gru.zr(hx).float()
+        h = h.float()
+        qs_in, ql_in = ops.gru_reset(zr_s, zr_l, h, x.float())
+        q_s = self.small_gru.convq(qs_in).float()
+        q_l = self.large_gru.convq(ql_in).float()
+        return ops.gru_blend(zr_s, zr_l, q_s, q_l, h, att.float())
 
 
 class BasicSelectiveMultiUpdateBlock(nn.Module):
