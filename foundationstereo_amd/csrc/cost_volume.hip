@@ -88,7 +88,35 @@ __global__ __launch_bounds__(kThreads) void gwc_kernel(const float* __restrict__
 
 // a1 + a2 + corr_stem[0] (1x1x1 conv 32 -> Cs):
 // out[b,o,d,h,w] = A[o,w] + [w>=d] Bm[o,w-d] + sum_g Wg[o,g] gwc_g(d,w)
-template <int G, int NOUT>
+//
+// Block = one (b,h) row x DC disparities.  Phase 1 walks the G groups: stage
+// the normalised group rows of fl/fr in LDS, each thread computes the group
+// correlation of VEC consecutive w for one d (one ds_read_b128 of L per
+// channel) into an LDS gwc tile [G][DC][W].  Phase 2 re-uses the staging
+// space for the A/Bm rows and emits all Cs output channels of VEC consecutive
+// w per item as 16-B stores (one 1-KiB coalesced store per wave-instruction).
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) v[j] = p[j];
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = v[j];
+  }
+}
+
+template <int G, int VEC>
 __global__ __launch_bounds__(kThreads) void comb_stem_kernel(const float* __restrict__ fl,
                                                              const float* __restrict__ fr,
                                                              const float* __restrict__ A,
@@ -103,59 +131,85 @@ __global__ __launch_bounds__(kThreads) void comb_stem_kernel(const float* __rest
   const int b = row / H, h = row - b * H;
   const int d0 = dc * DC, dn = min(DC, D - d0);
   const size_t plane = static_cast<size_t>(H) * W;
-
-  float acc[NOUT][G];
-#pragma unroll
-  for (int k = 0; k < NOUT; ++k)
-#pragma unroll
-    for (int g = 0; g < G; ++g) acc[k][g] = 0.f;
-
+  const int region0 = max(2 * Cg * W, 2 * Cs * W);
   float* L = smem;
   float* R = smem + Cg * W;
-#pragma unroll
+  float* gw = smem + region0;            // [G][DC][W]
+  float* Ws = gw + G * DC * W;           // [Cs][G]
+  const int nq = W / VEC;
+  const int items = dn * nq;
+
+  // ---- phase 1: group correlations into LDS
   for (int g = 0; g < G; ++g) {
     stage_group(fl, L, b, h, g, Cg, C, H, W);
     stage_group(fr, R, b, h, g, Cg, C, H, W);
+    for (int it = threadIdx.x; it < items; it += kThreads) {
+      const int dl = it / nq, q = it - dl * nq;
+      const int d = d0 + dl, w0 = q * VEC;
+      float acc[VEC];
+      int ri[VEC];
 #pragma unroll
-    for (int k = 0; k < NOUT; ++k) {
-      const int j = threadIdx.x + k * kThreads;
-      if (j < dn * W) {
-        const int dl = j / W, w = j - dl * W, d = d0 + dl;
-        if (w >= d) acc[k][g] = group_dot(L, R, Cg, W, w, d);
+      for (int j = 0; j < VEC; ++j) {
+        acc[j] = 0.f;
+        ri[j] = max(w0 + j - d, 0);  // clamped in-bounds; invalid lanes zeroed below
       }
+      for (int c = 0; c < Cg; ++c) {
+        float lv[VEC];
+        load_vec<VEC>(L + c * W + w0, lv);
+        const float* Rc = R + c * W;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += lv[j] * Rc[ri[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] = (w0 + j >= d) ? acc[j] : 0.f;
+      store_vec<VEC>(gw + (g * DC + dl) * W + w0, acc);
     }
     __syncthreads();
   }
 
-  // epilogue: stage A/Bm rows and the gwc columns of the stem weight
+  // ---- phase 2: stage A/Bm rows and the gwc columns of the stem weight, emit Cs channels
   float* As = smem;
   float* Bs = smem + Cs * W;
-  float* Ws = smem + 2 * Cs * W;
   const float* Ab = A + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
   const float* Bb = Bm + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
-  for (int i = threadIdx.x; i < Cs * W; i += kThreads) {
-    const int o = i / W, w = i - o * W;
-    As[i] = Ab[o * plane + w];
-    Bs[i] = Bb[o * plane + w];
+  for (int i = threadIdx.x; i < Cs * nq; i += kThreads) {
+    const int o = i / nq, q = i - o * nq;
+    float va[VEC], vb[VEC];
+    load_vec<VEC>(Ab + o * plane + q * VEC, va);
+    load_vec<VEC>(Bb + o * plane + q * VEC, vb);
+    store_vec<VEC>(As + o * W + q * VEC, va);
+    store_vec<VEC>(Bs + o * W + q * VEC, vb);
   }
   for (int i = threadIdx.x; i < Cs * G; i += kThreads) Ws[i] = Wg[i];
   __syncthreads();
 
+  for (int it = threadIdx.x; it < items; it += kThreads) {
+    const int dl = it / nq, q = it - dl * nq;
+    const int d = d0 + dl, w0 = q * VEC;
+    float gv[G][VEC];
 #pragma unroll
-  for (int k = 0; k < NOUT; ++k) {
-    const int j = threadIdx.x + k * kThreads;
-    if (j < dn * W) {
-      const int dl = j / W, w = j - dl * W, d = d0 + dl;
-      const bool valid = w >= d;
-      float* dst = out + (static_cast<size_t>(b) * Cs * D + d) * plane + static_cast<size_t>(h) * W + w;
-      for (int o = 0; o < Cs; ++o) {
-        float v = As[o * W + w];
-        if (valid) v += Bs[o * W + w - d];
+    for (int g = 0; g < G; ++g) load_vec<VEC>(gw + (g * DC + dl) * W + w0, gv[g]);
+    int bi[VEC];
+    bool ok[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      ok[j] = w0 + j >= d;
+      bi[j] = max(w0 + j - d, 0);
+    }
+    float* dst = out + (static_cast<size_t>(b) * Cs * D + d) * plane + static_cast<size_t>(h) * W + w0;
+    for (int o = 0; o < Cs; ++o) {
+      float v[VEC];
+      load_vec<VEC>(As + o * W + w0, v);
+      const float* Bo = Bs + o * W;
+      const float* wo = Ws + o * G;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
         float s = 0.f;
 #pragma unroll
-        for (int g = 0; g < G; ++g) s += Ws[o * G + g] * acc[k][g];
-        dst[static_cast<size_t>(o) * D * plane] = v + s;
+        for (int g = 0; g < G; ++g) s += wo[g] * gv[g][j];
+        v[j] = v[j] + (ok[j] ? Bo[bi[j]] : 0.f) + s;
       }
+      store_vec<VEC>(dst + static_cast<size_t>(o) * D * plane, v);
     }
   }
 }
@@ -202,11 +256,20 @@ __global__ __launch_bounds__(kThreads) void proj_kernel(const float* __restrict_
 #pragma unroll
   for (int o = 0; o < kProjO; ++o) acc[o] = 0.f;
   const float* xb = x + static_cast<size_t>(b) * C * P + p;
-  for (int c = 0; c < C; ++c) {
+  int c = 0;
+  for (; c + 8 <= C; c += 8) {  // 8 independent loads in flight per lane before the FMAs
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = xb[static_cast<size_t>(c + u) * P];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int o = 0; o < kProjO; ++o) acc[o] += wsm[o * C + c + u] * v[u];
+  }
+  for (; c < C; ++c) {
     const float v = xb[static_cast<size_t>(c) * P];
 #pragma unroll
-    for (int o = 0; o < kProjO; ++o)
-      if (o < on) acc[o] += wsm[o * C + c] * v;
+    for (int o = 0; o < kProjO; ++o) acc[o] += wsm[o * C + c] * v;
   }
 #pragma unroll
   for (int o = 0; o < kProjO; ++o)
@@ -265,20 +328,32 @@ int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, cons
   FSMI_CHECK_ARG(G == 8, "fsmi_comb_volume_stem: num_groups must be 8 (cv_group), got %d", G);
   FSMI_CHECK_ARG(C % G == 0, "C:%d, num_groups:%d", C, G);
   const int Cg = C / G;
-  const size_t lds = (static_cast<size_t>(std::max(2 * Cg * W, 2 * Cs * W)) + Cs * G) * sizeof(float);
+  // largest disparity chunk (<= 8) whose LDS image fits: staging/A-Bm rows + gwc tile + stem columns
+  auto lds_for = [&](int dc) {
+    return (static_cast<size_t>(std::max(2 * Cg * W, 2 * Cs * W)) + static_cast<size_t>(G) * dc * W + Cs * G) *
+           sizeof(float);
+  };
+  int DC = std::min(D, 8);
+  while (DC > 1 && lds_for(DC) > 160 * 1024) DC >>= 1;
+  const size_t lds = lds_for(DC);
   FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_comb_volume_stem: row too large for LDS (W=%d)", W);
-  const int DC = pick_dc(D, W);
   const int nDC = (D + DC - 1) / DC;
   const unsigned grid = static_cast<unsigned>(B) * H * nDC;
   hipStream_t s = as_stream(stream);
+  const bool vec = (W % 4) == 0;
+  const void* fn = vec ? reinterpret_cast<const void*>(comb_stem_kernel<8, 4>)
+                       : reinterpret_cast<const void*>(comb_stem_kernel<8, 1>);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(comb_stem_kernel<8, kNout>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     if (e != hipSuccess) return finish_launch("fsmi_comb_volume_stem: LDS attribute");
   }
   LaunchTimer t(FSMI_K_COMB, s);
-  hipLaunchKernelGGL((comb_stem_kernel<8, kNout>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs,
-                     D, H, W, DC, nDC);
+  if (vec)
+    hipLaunchKernelGGL((comb_stem_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D,
+                       H, W, DC, nDC);
+  else
+    hipLaunchKernelGGL((comb_stem_kernel<8, 1>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D,
+                       H, W, DC, nDC);
   return finish_launch("fsmi_comb_volume_stem");
 }
 

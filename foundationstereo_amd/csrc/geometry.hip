@@ -19,60 +19,69 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // Epilogue: D[i][j] in acc[r], i=(r&3)+8(r>>2)+4(l>>5), j=l&31; the pooled
 // levels average lane pairs (xor 1, 2, 4) -- the same (a+b)/2 as avg_pool2d.
 // ---------------------------------------------------------------------------
-constexpr int kCorrWaves = 4;
+// Block = (b, h, w1 tile) with one wave per w2 tile (blockDim = 64*T).  The
+// blocks of one row sit on one XCD (xcd_remap) so the R row is fetched from
+// HBM once and re-read from that L2.  Prologue: column norms of the w1 tile
+// and of the whole R row into LDS.  K loop: stage KC channels of the
+// normalised L tile and R row in LDS (x / max(|x|, eps), the F.normalize
+// division, once per element per block), then KC/2 MFMAs per wave with
+// conflict-free LDS operand reads.
+constexpr int kCorrKC = 16;
+constexpr int kCorrMaxT = 16;  // W <= 512
 
-__device__ __forceinline__ float column_norm(const float* __restrict__ f, size_t plane, int C, int w, bool ok,
-                                             int lane) {
-  float s = 0.f;
-  if (ok)
-    for (int c = lane >> 5; c < C; c += 2) {
-      const float v = f[c * plane + w];
-      s += v * v;
-    }
-  s += __shfl_xor(s, 32);
-  return fmaxf(sqrtf(s), 1e-12f);
-}
-
-__global__ __launch_bounds__(kCorrWaves * kWave) void allpairs_corr_kernel(
+__global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_kernel(
     const float* __restrict__ fl, const float* __restrict__ fr, float* __restrict__ lv0, float* __restrict__ lv1,
     float* __restrict__ lv2, float* __restrict__ lv3, int L, int C, int H, int W, int T) {
+  __shared__ __attribute__((aligned(16))) float As[kCorrKC][32];
+  __shared__ __attribute__((aligned(16))) float Bs[kCorrKC][kCorrMaxT * 32];
+  __shared__ float nA[32];
+  __shared__ float nB[kCorrMaxT * 32];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = blockIdx.x / T, t1 = blockIdx.x - row * T;
+  const int nthr = blockDim.x;
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = item / T, t1 = item - row * T;
   const int b = row / H, h = row - b * H;
   const size_t plane = static_cast<size_t>(H) * W;
   const float* L0 = fl + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
   const float* R0 = fr + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
-  const int i_l = lane & 31, k_l = lane >> 5;
-  const int w1 = t1 * 32 + i_l;
-  const bool ok1 = w1 < W;
-  const float na = column_norm(L0, plane, C, w1, ok1, lane);
+  const int WT = T * 32;
 
-  for (int t2 = wave; t2 < T; t2 += kCorrWaves) {
-    const int w2 = t2 * 32 + i_l;
-    const bool ok2 = w2 < W;
-    const float nb = column_norm(R0, plane, C, w2, ok2, lane);
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    int k0 = 0;
-    for (; k0 + 16 <= C; k0 += 16) {  // batch 8 k-steps of loads ahead of their MFMAs
-      float av[8], bv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int c = k0 + 2 * u + k_l;
-        av[u] = ok1 ? L0[c * plane + w1] / na : 0.f;
-        bv[u] = ok2 ? R0[c * plane + w2] / nb : 0.f;
+  // column norms: ||f[:, w]||_2 clamped at 1e-12 (F.normalize, core/geometry.py:75)
+  for (int j = threadIdx.x; j < 32 + WT; j += nthr) {
+    const bool isA = j < 32;
+    const int w = isA ? t1 * 32 + j : j - 32;
+    const float* f = isA ? L0 : R0;
+    float s = 0.f;
+    if (w < W)
+      for (int c = 0; c < C; ++c) {
+        const float v = f[c * plane + w];
+        s += v * v;
       }
+    const float n = fmaxf(sqrtf(s), 1e-12f);
+    if (isA) nA[j] = n; else nB[w] = n;
+  }
+
+  f32x16 acc;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int i_l = lane & 31, k_l = lane >> 5;
+  const int t2 = wave;
+  for (int k0 = 0; k0 < C; k0 += kCorrKC) {
+    __syncthreads();  // previous chunk consumed (and norms visible on the first pass)
+    for (int e = threadIdx.x; e < kCorrKC * 32; e += nthr) {
+      const int k = e >> 5, i = e & 31, c = k0 + k, w = t1 * 32 + i;
+      As[k][i] = (c < C && w < W) ? L0[c * plane + w] / nA[i] : 0.f;
     }
-    for (; k0 < C; k0 += 2) {
-      const int c = k0 + k_l;
-      const bool okc = c < C;
-      const float a = (ok1 && okc) ? L0[c * plane + w1] / na : 0.f;
-      const float bv = (ok2 && okc) ? R0[c * plane + w2] / nb : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+    for (int e = threadIdx.x; e < kCorrKC * WT; e += nthr) {
+      const int k = e / WT, w = e - k * WT, c = k0 + k;
+      Bs[k][w] = (c < C && w < W) ? R0[c * plane + w] / nB[w] : 0.f;
     }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kCorrKC; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[kk + k_l][i_l], Bs[kk + k_l][t2 * 32 + i_l], acc, 0, 0, 0);
+  }
+  {
     // epilogue: rows i (w1) in registers, columns j (w2) on lanes
     const int j = lane & 31;
     const size_t rowbase = static_cast<size_t>(b) * H + h;
@@ -174,31 +183,47 @@ __device__ __forceinline__ float unnorm(float x, int n) {
   return (xn + 1.f) * (static_cast<float>(n - 1) / 2.f);
 }
 
+// The 2r+1 taps of one (pixel, level): window base, per-tap fraction and which
+// window pair each tap reads.  Channel-independent, so computed once and
+// reused for every channel of the level (the division lives here).
 template <int R>
-__device__ __forceinline__ void sample_taps(const float* __restrict__ src, size_t stride, int n, float xc,
-                                            float* __restrict__ dst, size_t dstride) {
+struct Taps {
+  static constexpr int K = 2 * R + 1, NW = 2 * R + 4;
+  int xb;            // window covers [xb, xb + NW)
+  float f[K];        // fraction of tap k
+  int sel[K];        // tap k interpolates win[k+sel], win[k+sel+1], sel in {0,1,2}
+
+  __device__ __forceinline__ void init(float xc, int n) {
 #pragma clang fp contract(off)
-  constexpr int K = 2 * R + 1, NW = 2 * R + 4;
-  // xc = centre coordinate (tap k sits at xc + (k - R)); clamp keeps int math defined
-  const float xcl = fminf(fmaxf(xc, -1.0e6f), 1.0e6f);
-  const int xb = static_cast<int>(floorf(xcl)) - R - 1;
-  float win[NW];
+    // xc = centre coordinate (tap k sits at xc + (k - R)); clamp keeps int math defined
+    const float xcl = fminf(fmaxf(xc, -1.0e6f), 1.0e6f);
+    xb = static_cast<int>(floorf(xcl)) - R - 1;
 #pragma unroll
-  for (int j = 0; j < NW; ++j) {
-    const int x = xb + j;
-    win[j] = (x >= 0 && x < n) ? src[static_cast<size_t>(x) * stride] : 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float ix = unnorm(static_cast<float>(k - R) + xcl, n);
+      const float fl = floorf(ix);
+      f[k] = ix - fl;
+      sel[k] = static_cast<int>(fl) - xb - k;
+    }
   }
+
+  __device__ __forceinline__ void sample(const float* __restrict__ src, size_t stride, int n,
+                                         float* __restrict__ dst, size_t dstride) const {
+#pragma clang fp contract(off)
+    float win[NW];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const float ix = unnorm(static_cast<float>(k - R) + xcl, n);
-    const float fl = floorf(ix);
-    const float f = ix - fl;
-    const int sel = static_cast<int>(fl) - xb - k;  // in {0,1,2}
-    const float v0 = sel == 0 ? win[k] : (sel == 1 ? win[k + 1] : win[k + 2]);
-    const float v1 = sel == 0 ? win[k + 1] : (sel == 1 ? win[k + 2] : win[k + 3]);
-    dst[static_cast<size_t>(k) * dstride] = v0 * (1.f - f) + v1 * f;
+    for (int j = 0; j < NW; ++j) {
+      const int x = xb + j;
+      win[j] = (x >= 0 && x < n) ? src[static_cast<size_t>(x) * stride] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float v0 = sel[k] == 0 ? win[k] : (sel[k] == 1 ? win[k + 1] : win[k + 2]);
+      const float v1 = sel[k] == 0 ? win[k + 1] : (sel[k] == 1 ? win[k + 2] : win[k + 3]);
+      dst[static_cast<size_t>(k) * dstride] = v0 * (1.f - f[k]) + v1 * f[k];
+    }
   }
-}
+};
 
 template <int R>
 __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
@@ -219,18 +244,26 @@ __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
   const int CH = a.L * K * (a.Cv + 1);
   const int base = i * K * (a.Cv + 1);
   float* outp = a.out + static_cast<size_t>(b) * CH * HW + hw;
+  Taps<R> tp;
   if (chunk < nchunk_geo) {
     const int Di = a.D >> i;
+    tp.init(ds, Di);
     const float* vol = a.vol[i] + static_cast<size_t>(b) * a.Cv * Di * HW + hw;
-    const int c0 = chunk * kCPC, c1 = min(a.Cv, c0 + kCPC);
-    for (int c = c0; c < c1; ++c)
-      sample_taps<R>(vol + static_cast<size_t>(c) * Di * HW, HW, Di, ds,
-                     outp + static_cast<size_t>(base + c * K) * HW, HW);
+    const int c0 = chunk * kCPC;
+    if (c0 + kCPC <= a.Cv) {
+#pragma unroll
+      for (int u = 0; u < kCPC; ++u)
+        tp.sample(vol + static_cast<size_t>(c0 + u) * Di * HW, HW, Di,
+                  outp + static_cast<size_t>(base + (c0 + u) * K) * HW, HW);
+    } else {
+      for (int c = c0; c < a.Cv; ++c)
+        tp.sample(vol + static_cast<size_t>(c) * Di * HW, HW, Di, outp + static_cast<size_t>(base + c * K) * HW, HW);
+    }
   } else {
     const int W2i = a.W2 >> i;
     const float* row = a.cor[i] + static_cast<size_t>(p) * W2i;
-    const float xc = static_cast<float>(w) / s - ds;
-    sample_taps<R>(row, 1, W2i, xc, outp + static_cast<size_t>(base + a.Cv * K) * HW, HW);
+    tp.init(static_cast<float>(w) / s - ds, W2i);
+    tp.sample(row, 1, W2i, outp + static_cast<size_t>(base + a.Cv * K) * HW, HW);
   }
 }
 
@@ -268,12 +301,13 @@ int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, i
   FSMI_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0, "fsmi_allpairs_corr: bad shape");
   for (int i = 0; i < num_levels; ++i) FSMI_CHECK_ARG(levels[i], "fsmi_allpairs_corr: null level %d", i);
   const int T = (W + 31) / 32;
+  FSMI_CHECK_ARG(T <= kCorrMaxT, "fsmi_allpairs_corr: W=%d exceeds %d", W, kCorrMaxT * 32);
   float* lv[4] = {levels[0], nullptr, nullptr, nullptr};
   for (int i = 1; i < num_levels; ++i) lv[i] = levels[i];
   for (int i = num_levels; i < 4; ++i) lv[i] = lv[0];
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_CORR, s);
-  hipLaunchKernelGGL(allpairs_corr_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(kCorrWaves * kWave), 0, s,
+  hipLaunchKernelGGL(allpairs_corr_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
                      fl, fr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);
   return finish_launch("fsmi_allpairs_corr");
 }

@@ -12,7 +12,7 @@ constexpr int kT = 256;
 // core/submodule.py:431-435: sum_d d * p_d
 __global__ __launch_bounds__(kT) void regression_kernel(const float* __restrict__ prob, float* __restrict__ out,
                                                         int D, int HW, long long P) {
-  const long long p = blockIdx.x * static_cast<long long>(kT) + threadIdx.x;
+  const long long p = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
   if (p >= P) return;
   const long long b = p / HW;
   const int hw = static_cast<int>(p - b * HW);
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kT) void regression_kernel(const float* __restrict_
 // Same op order as the reference: p_d = exp(x_d - max) / sum, then sum d*p_d.
 __global__ __launch_bounds__(kT) void softmax_regression_kernel(const float* __restrict__ logit,
                                                                 float* __restrict__ out, int D, int HW, long long P) {
-  const long long p = blockIdx.x * static_cast<long long>(kT) + threadIdx.x;
+  const long long p = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
   if (p >= P) return;
   const long long b = p / HW;
   const int hw = static_cast<int>(p - b * HW);
@@ -46,7 +46,7 @@ template <bool SOFTMAX>
 __global__ __launch_bounds__(kT) void upsample_kernel(const float* __restrict__ disp, const float* __restrict__ wts,
                                                       float* __restrict__ out, float scale, int h, int w,
                                                       long long P) {
-  const long long p = blockIdx.x * static_cast<long long>(kT) + threadIdx.x;
+  const long long p = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
   if (p >= P) return;
   const int W4 = 4 * w, H4 = 4 * h;
   const long long HW4 = static_cast<long long>(H4) * W4;
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kT) void gru_reset_kernel(const float* __restrict__
                                                        const float* __restrict__ h, const float* __restrict__ x,
                                                        float* __restrict__ qs, float* __restrict__ ql, int Hd, int Cx,
                                                        int HW, long long total) {
-  const long long i = blockIdx.x * static_cast<long long>(kT) + threadIdx.x;
+  const long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
   if (i >= total) return;
   const int Ct = Hd + Cx;
   const int hw = static_cast<int>(i % HW);
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kT) void gru_blend_kernel(const float* __restrict__
                                                        const float* __restrict__ q_s, const float* __restrict__ q_l,
                                                        const float* h, const float* __restrict__ att, float* hout,
                                                        int Hd, int HW, long long total) {
-  const long long i = blockIdx.x * static_cast<long long>(kT) + threadIdx.x;
+  const long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
   if (i >= total) return;
   const int hw = static_cast<int>(i % HW);
   const long long r = i / HW;
@@ -141,7 +141,7 @@ int fsmi_disparity_regression(const float* prob, float* out, int B, int D, int H
   const long long P = static_cast<long long>(B) * H * W;
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_REG, s);
-  hipLaunchKernelGGL(regression_kernel, dim3(ceil_div(P, kT)), dim3(kT), 0, s, prob, out, D, H * W, P);
+  hipLaunchKernelGGL(regression_kernel, dim3(ceil_div(P, 64)), dim3(64), 0, s, prob, out, D, H * W, P);
   return finish_launch("fsmi_disparity_regression");
 }
 
@@ -151,7 +151,8 @@ int fsmi_softmax_regression(const float* logits, float* out, int B, int D, int H
   const long long P = static_cast<long long>(B) * H * W;
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_REG, s);
-  hipLaunchKernelGGL(softmax_regression_kernel, dim3(ceil_div(P, kT)), dim3(kT), 0, s, logits, out, D, H * W, P);
+  // 64-thread blocks: one pixel per lane, so a 19k-pixel plane still spreads over every CU
+  hipLaunchKernelGGL(softmax_regression_kernel, dim3(ceil_div(P, 64)), dim3(64), 0, s, logits, out, D, H * W, P);
   return finish_launch("fsmi_softmax_regression");
 }
 

@@ -33,8 +33,9 @@ _MEAN = (0.485, 0.456, 0.406)
 _STD = (0.229, 0.224, 0.225)
 
 
-def autocast(enabled):
-    return torch.autocast("cuda", dtype=torch.float16, enabled=bool(enabled))
+def autocast(enabled, dtype="float16"):
+    """``torch.cuda.amp.autocast(enabled)`` of the reference (fp16); ``mixed_dtype`` may select bf16."""
+    return torch.autocast("cuda", dtype=getattr(torch, dtype), enabled=bool(enabled))
 
 
 def normalize_image(img):
@@ -178,7 +179,7 @@ class FoundationStereo(nn.Module):
 
     def upsample_disp(self, disp, mask_feat_4, stem_2x):
         """core/foundation_stereo.py:183-191: returns (B,1,H,W) fp32."""
-        with autocast(self.args.mixed_precision):
+        with autocast(self.args.mixed_precision, self.args.get("mixed_dtype", "float16")):
             xspx = self.spx_2_gru(mask_feat_4, stem_2x)
             logits = self.spx_gru(xspx)
         return ops.softmax_context_upsample(disp.float(), logits.float(), 4.0).unsqueeze(1)
@@ -188,7 +189,8 @@ class FoundationStereo(nn.Module):
         image1 = normalize_image(image1)
         image2 = normalize_image(image2)
         mp = self.args.mixed_precision
-        with autocast(mp):
+        md = self.args.get("mixed_dtype", "float16")
+        with autocast(mp, md):
             features_left, features_right, vit_feat = self._backbone(image1, image2)
             stem_2x = self.stem_2(image1)
             vol = self.build_stem_volume(features_left[0], features_right[0])
@@ -212,7 +214,7 @@ class FoundationStereo(nn.Module):
         for itr in range(iters):
             disp = disp.detach()
             geo_feat = geo_fn(disp)
-            with autocast(mp):
+            with autocast(mp, md):
                 net_list, mask_feat_4, delta_disp = self.update_block(net_list, inp_list, geo_feat, disp, att)
             disp = disp + delta_disp.float()
             if test_mode and itr < iters - 1:
