@@ -23,9 +23,9 @@ SIGNATURES = {
     "fsmi_arch": [],
     "fsmi_gwc_volume": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_concat_volume": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "fsmi_comb_volume_stem": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_comb_volume_stem": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_pointwise_proj": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "fsmi_allpairs_corr": [_P, _P, _PP, _I, _I, _I, _I, _I, _P],
+    "fsmi_allpairs_corr": [_P, _P, _PP, _I, _I, _I, _I, _I, _P, _P],
     "fsmi_volume_pyramid": [_P, _PP, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_geo_lookup": [_PP, _PP, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_bilinear_sampler_1d": [_P, _P, _P, _I, _I, _I, _I, _P],
@@ -35,13 +35,14 @@ SIGNATURES = {
     "fsmi_softmax_context_upsample": [_P, _P, _P, _F, _I, _I, _I, _P],
     "fsmi_gru_reset": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_gru_blend": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "fsmi_conv3d_direct": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
-           "gru_reset", "gru_blend"]
+           "gru_reset", "gru_blend", "conv3d"]
 
 _lib = None
 

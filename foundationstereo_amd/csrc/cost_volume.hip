@@ -50,6 +50,27 @@ __device__ __forceinline__ void stage_group(const float* __restrict__ f, float* 
   __syncthreads();
 }
 
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) v[j] = p[j];
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = v[j];
+  }
+}
+
 __device__ __forceinline__ float group_dot(const float* L, const float* R, int Cg, int W, int w, int d) {
   float v = 0.f;
   for (int c = 0; c < Cg; ++c) v += L[c * W + w] * R[c * W + (w - d)];
@@ -86,6 +107,114 @@ __global__ __launch_bounds__(kThreads) void gwc_kernel(const float* __restrict__
   }
 }
 
+// a1, vector path (D % 4 == 0, W % 4 == 0): block = one (b, h, g), the group's
+// two rows staged + normalised ONCE, every thread owns a 4(d) x 4(w) output
+// block: per channel one ds_read_b128 of L and a 7-wide window of R feed 16
+// FMAs (vs 2 LDS reads per FMA), and the block writes 4 x 16-B per item.
+__global__ __launch_bounds__(kThreads) void gwc_tile_kernel(const float* __restrict__ fl,
+                                                            const float* __restrict__ fr, float* __restrict__ out,
+                                                            int C, int G, int D, int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Cg = C / G;
+  float* L = smem;
+  float* R = smem + Cg * W;
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int g = item % G;
+  const int row = item / G;
+  const int b = row / H, h = row - b * H;
+  const size_t plane = static_cast<size_t>(H) * W;
+  stage_group(fl, L, b, h, g, Cg, C, H, W);
+  stage_group(fr, R, b, h, g, Cg, C, H, W);
+  const int nwq = W >> 2, items = (D >> 2) * nwq;
+  for (int it = threadIdx.x; it < items; it += kThreads) {
+    const int dq = it / nwq, wq = it - dq * nwq;
+    const int d0 = dq * 4, w0 = wq * 4;
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    // window index t = j - i + 3 in [0,7): R[w0 + j - d0 - i] = R[w0 - d0 - 3 + t]
+    int ridx[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) ridx[t] = max(w0 - d0 - 3 + t, 0);
+    for (int c = 0; c < Cg; ++c) {
+      const float4 l4 = *reinterpret_cast<const float4*>(L + c * W + w0);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+      const float* Rc = R + c * W;
+      float rv[7];
+#pragma unroll
+      for (int t = 0; t < 7; ++t) rv[t] = Rc[ridx[t]];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += lv[j] * rv[j - i + 3];
+    }
+    float* dst = out + ((static_cast<size_t>(b) * G + g) * D + d0) * plane + static_cast<size_t>(h) * W + w0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = d0 + i;
+      float4 v;
+      v.x = (w0 + 0 >= d) ? acc[i][0] : 0.f;
+      v.y = (w0 + 1 >= d) ? acc[i][1] : 0.f;
+      v.z = (w0 + 2 >= d) ? acc[i][2] : 0.f;
+      v.w = (w0 + 3 >= d) ? acc[i][3] : 0.f;
+      *reinterpret_cast<float4*>(dst + static_cast<size_t>(i) * plane) = v;
+    }
+  }
+}
+
+// corr_stem[0] applied to [gwc | concat] as a pure stream (the fused build's
+// second half): thread = (b, d, h, VEC consecutive w); reads the G gwc values
+// (coalesced), the L2-resident A/Bm rows, writes Cs channels as 16-B stores.
+// out[b,o,d,h,w] = A[b,o,h,w] + [w>=d] Bm[b,o,h,w-d] + sum_g Wg[o,g] gwc[b,g,d,h,w]
+template <int G, int VEC>
+__global__ __launch_bounds__(kThreads) void stem_stream_kernel(const float* __restrict__ gwc,
+                                                               const float* __restrict__ A,
+                                                               const float* __restrict__ Bm,
+                                                               const float* __restrict__ Wg, float* __restrict__ out,
+                                                               int Cs, int D, int H, int W, long long total) {
+  const long long t = blockIdx.x * static_cast<long long>(kThreads) + threadIdx.x;
+  if (t >= total) return;
+  const int nq = W / VEC;
+  const int q = static_cast<int>(t % nq);
+  long long r = t / nq;
+  const int h = static_cast<int>(r % H);
+  r /= H;
+  const int d = static_cast<int>(r % D);
+  const int b = static_cast<int>(r / D);
+  const int w0 = q * VEC;
+  const size_t plane = static_cast<size_t>(H) * W;
+  const size_t hw = static_cast<size_t>(h) * W + w0;
+  float gv[G][VEC];
+#pragma unroll
+  for (int g = 0; g < G; ++g) load_vec<VEC>(gwc + ((static_cast<size_t>(b) * G + g) * D + d) * plane + hw, gv[g]);
+  bool ok[VEC];
+  int bi[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    ok[j] = w0 + j >= d;
+    bi[j] = max(w0 + j - d, 0);
+  }
+  const float* Ab = A + static_cast<size_t>(b) * Cs * plane + hw;
+  const float* Bb = Bm + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
+  float* dst = out + (static_cast<size_t>(b) * Cs * D + d) * plane + hw;
+  for (int o = 0; o < Cs; ++o) {
+    float v[VEC];
+    load_vec<VEC>(Ab + o * plane, v);
+    const float* Bo = Bb + o * plane;
+    const float* wo = Wg + o * G;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g) s += wo[g] * gv[g][j];
+      v[j] = v[j] + (ok[j] ? Bo[bi[j]] : 0.f) + s;
+    }
+    store_vec<VEC>(dst + static_cast<size_t>(o) * D * plane, v);
+  }
+}
+
 // a1 + a2 + corr_stem[0] (1x1x1 conv 32 -> Cs):
 // out[b,o,d,h,w] = A[o,w] + [w>=d] Bm[o,w-d] + sum_g Wg[o,g] gwc_g(d,w)
 //
@@ -95,27 +224,6 @@ __global__ __launch_bounds__(kThreads) void gwc_kernel(const float* __restrict__
 // channel) into an LDS gwc tile [G][DC][W].  Phase 2 re-uses the staging
 // space for the A/Bm rows and emits all Cs output channels of VEC consecutive
 // w per item as 16-B stores (one 1-KiB coalesced store per wave-instruction).
-template <int VEC>
-__device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    const float4 t = *reinterpret_cast<const float4*>(p);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-  } else {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) v[j] = p[j];
-  }
-}
-
-template <int VEC>
-__device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) p[j] = v[j];
-  }
-}
-
 template <int G, int VEC>
 __global__ __launch_bounds__(kThreads) void comb_stem_kernel(const float* __restrict__ fl,
                                                              const float* __restrict__ fr,
@@ -280,6 +388,32 @@ constexpr int kNout = 8;
 
 inline int pick_dc(int D, int W) { return max(1, min(D, kNout * kThreads / W)); }
 
+// gwc volume into `out` (B,G,D,H,W): the 4x4-blocked tile kernel when D and W
+// are multiples of 4, else the general per-output kernel.
+int launch_gwc(const float* fl, const float* fr, float* out, int B, int C, int G, int D, int H, int W,
+               hipStream_t s) {
+  const int Cg = C / G;
+  const size_t lds = static_cast<size_t>(2) * Cg * W * sizeof(float);
+  FSMI_CHECK_ARG(lds <= 160 * 1024, "gwc volume: row too large for LDS (Cg=%d W=%d)", Cg, W);
+  const bool tile = (D % 4 == 0) && (W % 4 == 0);
+  const void* fn = tile ? reinterpret_cast<const void*>(gwc_tile_kernel)
+                        : reinterpret_cast<const void*>(gwc_kernel<kNout>);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return finish_launch("gwc volume: LDS attribute");
+  }
+  if (tile) {
+    hipLaunchKernelGGL(gwc_tile_kernel, dim3(static_cast<unsigned>(B) * H * G), dim3(kThreads), lds, s, fl, fr, out,
+                       C, G, D, H, W);
+  } else {
+    const int DC = pick_dc(D, W);
+    const int nDC = (D + DC - 1) / DC;
+    hipLaunchKernelGGL(gwc_kernel<kNout>, dim3(static_cast<unsigned>(B) * H * nDC), dim3(kThreads), lds, s, fl, fr,
+                       out, C, G, D, H, W, DC, nDC);
+  }
+  return finish_launch("gwc volume");
+}
+
 }  // namespace
 }  // namespace fsmi
 
@@ -292,21 +426,9 @@ int fsmi_gwc_volume(const float* fl, const float* fr, float* out, int B, int C, 
   FSMI_CHECK_ARG(fl && fr && out, "fsmi_gwc_volume: null pointer");
   FSMI_CHECK_ARG(B > 0 && C > 0 && G > 0 && D > 0 && H > 0 && W > 0, "fsmi_gwc_volume: bad shape");
   FSMI_CHECK_ARG(C % G == 0, "C:%d, num_groups:%d", C, G);
-  const int Cg = C / G;
-  const size_t lds = static_cast<size_t>(2) * Cg * W * sizeof(float);
-  FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_gwc_volume: row too large for LDS (Cg=%d W=%d)", Cg, W);
-  const int DC = pick_dc(D, W);
-  const int nDC = (D + DC - 1) / DC;
-  const unsigned grid = static_cast<unsigned>(B) * H * nDC;
   hipStream_t s = as_stream(stream);
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(gwc_kernel<kNout>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    if (e != hipSuccess) return finish_launch("fsmi_gwc_volume: LDS attribute");
-  }
   LaunchTimer t(FSMI_K_GWC, s);
-  hipLaunchKernelGGL(gwc_kernel<kNout>, dim3(grid), dim3(kThreads), lds, s, fl, fr, out, C, G, D, H, W, DC, nDC);
-  return finish_launch("fsmi_gwc_volume");
+  return launch_gwc(fl, fr, out, B, C, G, D, H, W, s);
 }
 
 int fsmi_concat_volume(const float* pl, const float* pr, float* out, int B, int C, int D, int H, int W,
@@ -322,11 +444,26 @@ int fsmi_concat_volume(const float* pl, const float* pr, float* out, int B, int 
 }
 
 int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, const float* Bm, const float* Wg,
-                          float* out, int B, int C, int G, int Cs, int D, int H, int W, void* stream) {
+                          float* gwc_ws, float* out, int B, int C, int G, int Cs, int D, int H, int W, void* stream) {
   FSMI_CHECK_ARG(fl && fr && A && Bm && Wg && out, "fsmi_comb_volume_stem: null pointer");
   FSMI_CHECK_ARG(B > 0 && C > 0 && Cs > 0 && D > 0 && H > 0 && W > 0, "fsmi_comb_volume_stem: bad shape");
   FSMI_CHECK_ARG(G == 8, "fsmi_comb_volume_stem: num_groups must be 8 (cv_group), got %d", G);
   FSMI_CHECK_ARG(C % G == 0, "C:%d, num_groups:%d", C, G);
+  if (gwc_ws) {  // two streaming passes: gwc tile kernel -> workspace, then the stem stream
+    hipStream_t s = as_stream(stream);
+    LaunchTimer t(FSMI_K_COMB, s);
+    const int rc = launch_gwc(fl, fr, gwc_ws, B, C, G, D, H, W, s);
+    if (rc) return rc;
+    const bool vec = (W % 4) == 0;
+    const long long total = static_cast<long long>(B) * D * H * (vec ? W / 4 : W);
+    if (vec)
+      hipLaunchKernelGGL((stem_stream_kernel<8, 4>), dim3(ceil_div(total, kThreads)), dim3(kThreads), 0, s, gwc_ws, A,
+                         Bm, Wg, out, Cs, D, H, W, total);
+    else
+      hipLaunchKernelGGL((stem_stream_kernel<8, 1>), dim3(ceil_div(total, kThreads)), dim3(kThreads), 0, s, gwc_ws, A,
+                         Bm, Wg, out, Cs, D, H, W, total);
+    return finish_launch("fsmi_comb_volume_stem");
+  }
   const int Cg = C / G;
   // largest disparity chunk (<= 8) whose LDS image fits: staging/A-Bm rows + gwc tile + stem columns
   auto lds_for = [&](int dc) {

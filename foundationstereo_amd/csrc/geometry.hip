@@ -29,6 +29,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kCorrKC = 16;
 constexpr int kCorrMaxT = 16;  // W <= 512
 
+__device__ __forceinline__ void corr_epilogue(const f32x16& acc, float* __restrict__ lv0, float* __restrict__ lv1,
+                                              float* __restrict__ lv2, float* __restrict__ lv3, int L, int H, int W,
+                                              int b, int h, int t1, int t2, int lane);
+
 __global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_kernel(
     const float* __restrict__ fl, const float* __restrict__ fr, float* __restrict__ lv0, float* __restrict__ lv1,
     float* __restrict__ lv2, float* __restrict__ lv3, int L, int C, int H, int W, int T) {
@@ -81,36 +85,117 @@ __global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_kernel(
     for (int kk = 0; kk < kCorrKC; kk += 2)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[kk + k_l][i_l], Bs[kk + k_l][t2 * 32 + i_l], acc, 0, 0, 0);
   }
-  {
-    // epilogue: rows i (w1) in registers, columns j (w2) on lanes
-    const int j = lane & 31;
-    const size_t rowbase = static_cast<size_t>(b) * H + h;
-    const int W1 = W >> 1, W2 = W >> 2, W3 = W >> 3;
+  corr_epilogue(acc, lv0, lv1, lv2, lv3, L, H, W, b, h, t1, t2, lane);
+}
+
+// Epilogue shared by both all-pairs variants: D[i][j] in acc[r] with
+// i=(r&3)+8(r>>2)+4(l>>5) (w1), j=l&31 (w2); pooled levels by lane-pair shuffles.
+__device__ __forceinline__ void corr_epilogue(const f32x16& acc, float* __restrict__ lv0, float* __restrict__ lv1,
+                                              float* __restrict__ lv2, float* __restrict__ lv3, int L, int H, int W,
+                                              int b, int h, int t1, int t2, int lane) {
+  const int j = lane & 31;
+  const size_t rowbase = static_cast<size_t>(b) * H + h;
+  const int W1 = W >> 1, W2 = W >> 2, W3 = W >> 3;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int gw1 = t1 * 32 + i;
-      const bool okr = gw1 < W;
-      float v = acc[r];
-      const int gw2 = t2 * 32 + j;
-      if (okr && gw2 < W) lv0[(rowbase * W + gw1) * W + gw2] = v;
-      if (L > 1) {
-        v = (v + __shfl_xor(v, 1)) / 2.f;
-        const int c1 = t2 * 16 + (j >> 1);
-        if (okr && (j & 1) == 0 && c1 < W1) lv1[(rowbase * W + gw1) * W1 + c1] = v;
-        if (L > 2) {
-          v = (v + __shfl_xor(v, 2)) / 2.f;
-          const int c2 = t2 * 8 + (j >> 2);
-          if (okr && (j & 3) == 0 && c2 < W2) lv2[(rowbase * W + gw1) * W2 + c2] = v;
-          if (L > 3) {
-            v = (v + __shfl_xor(v, 4)) / 2.f;
-            const int c3 = t2 * 4 + (j >> 3);
-            if (okr && (j & 7) == 0 && c3 < W3) lv3[(rowbase * W + gw1) * W3 + c3] = v;
-          }
+  for (int r = 0; r < 16; ++r) {
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int gw1 = t1 * 32 + i;
+    const bool okr = gw1 < W;
+    float v = acc[r];
+    const int gw2 = t2 * 32 + j;
+    if (okr && gw2 < W) lv0[(rowbase * W + gw1) * W + gw2] = v;
+    if (L > 1) {
+      v = (v + __shfl_xor(v, 1)) / 2.f;
+      const int c1 = t2 * 16 + (j >> 1);
+      if (okr && (j & 1) == 0 && c1 < W1) lv1[(rowbase * W + gw1) * W1 + c1] = v;
+      if (L > 2) {
+        v = (v + __shfl_xor(v, 2)) / 2.f;
+        const int c2 = t2 * 8 + (j >> 2);
+        if (okr && (j & 3) == 0 && c2 < W2) lv2[(rowbase * W + gw1) * W2 + c2] = v;
+        if (L > 3) {
+          v = (v + __shfl_xor(v, 4)) / 2.f;
+          const int c3 = t2 * 4 + (j >> 3);
+          if (okr && (j & 7) == 0 && c3 < W3) lv3[(rowbase * W + gw1) * W3 + c3] = v;
         }
       }
     }
   }
+}
+
+// F.normalize over channels (core/geometry.py:75) into a workspace, one thread
+// per pixel: out[b,c,p] = f[b,c,p] / max(||f[b,:,p]||_2, 1e-12).  grid.y picks fl / fr.
+__global__ __launch_bounds__(256) void normalize_cols_kernel(const float* __restrict__ f0,
+                                                             const float* __restrict__ f1, float* __restrict__ o0,
+                                                             float* __restrict__ o1, int C, int HW, long long P) {
+  const long long p = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
+  if (p >= P) return;
+  const float* f = blockIdx.y ? f1 : f0;
+  float* o = blockIdx.y ? o1 : o0;
+  const long long b = p / HW;
+  const size_t base = static_cast<size_t>(b) * C * HW + static_cast<size_t>(p - b * HW);
+  float s = 0.f;
+  int c = 0;
+  for (; c + 8 <= C; c += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = f[base + static_cast<size_t>(c + u) * HW];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u] * v[u];
+  }
+  for (; c < C; ++c) {
+    const float v = f[base + static_cast<size_t>(c) * HW];
+    s += v * v;
+  }
+  const float n = fmaxf(sqrtf(s), 1e-12f);
+  for (c = 0; c + 8 <= C; c += 8) {  // second pass (L2-hot), again 8 loads in flight per lane
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = f[base + static_cast<size_t>(c + u) * HW];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) o[base + static_cast<size_t>(c + u) * HW] = v[u] / n;
+  }
+  for (; c < C; ++c) o[base + static_cast<size_t>(c) * HW] = f[base + static_cast<size_t>(c) * HW] / n;
+}
+
+// all-pairs on pre-normalised operands: no LDS, no barriers.  Block = (b, h,
+// w1 tile), one wave per w2 tile; each wave streams its two 32-column slabs
+// from L2 (row-major blocks of a row share one XCD) 16 k-steps of loads ahead
+// of the MFMAs that consume them.
+__global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_direct_kernel(
+    const float* __restrict__ nl, const float* __restrict__ nr, float* __restrict__ lv0, float* __restrict__ lv1,
+    float* __restrict__ lv2, float* __restrict__ lv3, int L, int C, int H, int W, int T) {
+  const int lane = threadIdx.x & 63, t2 = threadIdx.x >> 6;
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = item / T, t1 = item - row * T;
+  const int b = row / H, h = row - b * H;
+  const size_t plane = static_cast<size_t>(H) * W;
+  const int i_l = lane & 31, k_l = lane >> 5;
+  const int w1 = t1 * 32 + i_l, w2 = t2 * 32 + i_l;
+  const bool ok1 = w1 < W, ok2 = w2 < W;
+  const float* A0 = nl + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W + (ok1 ? w1 : 0);
+  const float* B0 = nr + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W + (ok2 ? w2 : 0);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  int k0 = 0;
+  for (; k0 + 32 <= C; k0 += 32) {
+    float av[16], bv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const size_t off = static_cast<size_t>(k0 + 2 * u + k_l) * plane;
+      av[u] = ok1 ? A0[off] : 0.f;
+      bv[u] = ok2 ? B0[off] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+  for (; k0 < C; k0 += 2) {
+    const int c = k0 + k_l;
+    const float a = (ok1 && c < C) ? A0[static_cast<size_t>(c) * plane] : 0.f;
+    const float bb = (ok2 && c < C) ? B0[static_cast<size_t>(c) * plane] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc, 0, 0, 0);
+  }
+  corr_epilogue(acc, lv0, lv1, lv2, lv3, L, H, W, b, h, t1, t2, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -192,6 +277,7 @@ struct Taps {
   int xb;            // window covers [xb, xb + NW)
   float f[K];        // fraction of tap k
   int sel[K];        // tap k interpolates win[k+sel], win[k+sel+1], sel in {0,1,2}
+  bool lo, hi;       // window ends needed (only when a tap's round trip crossed an integer)
 
   __device__ __forceinline__ void init(float xc, int n) {
 #pragma clang fp contract(off)
@@ -205,16 +291,21 @@ struct Taps {
       f[k] = ix - fl;
       sel[k] = static_cast<int>(fl) - xb - k;
     }
+    lo = sel[0] == 0;       // only tap 0 can reach win[0]
+    hi = sel[K - 1] == 2;   // only tap 2r can reach win[2r+3]
   }
 
   __device__ __forceinline__ void sample(const float* __restrict__ src, size_t stride, int n,
                                          float* __restrict__ dst, size_t dstride) const {
 #pragma clang fp contract(off)
+    // the 2r+2 window elements every tap set touches, plus the two ends only for lanes whose
+    // taps need them: HBM sees the algorithmic 2r+2 loads per channel
     float win[NW];
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int x = xb + j;
-      win[j] = (x >= 0 && x < n) ? src[static_cast<size_t>(x) * stride] : 0.f;
+      const bool need = (j == 0) ? lo : ((j == NW - 1) ? hi : true);
+      win[j] = (need && x >= 0 && x < n) ? src[static_cast<size_t>(x) * stride] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -295,7 +386,7 @@ using namespace fsmi;
 extern "C" {
 
 int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, int num_levels, int B, int C, int H,
-                       int W, void* stream) {
+                       int W, float* ws, void* stream) {
   FSMI_CHECK_ARG(fl && fr && levels, "fsmi_allpairs_corr: null pointer");
   FSMI_CHECK_ARG(num_levels >= 1 && num_levels <= FSMI_MAX_LEVELS, "fsmi_allpairs_corr: num_levels %d", num_levels);
   FSMI_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0, "fsmi_allpairs_corr: bad shape");
@@ -307,8 +398,17 @@ int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, i
   for (int i = num_levels; i < 4; ++i) lv[i] = lv[0];
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_CORR, s);
-  hipLaunchKernelGGL(allpairs_corr_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
-                     fl, fr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);
+  if (ws) {  // normalise once into the workspace, then the barrier-free MFMA pass
+    const long long P = static_cast<long long>(B) * H * W;
+    float* nl = ws;
+    float* nr = ws + static_cast<size_t>(B) * C * H * W;
+    hipLaunchKernelGGL(normalize_cols_kernel, dim3(ceil_div(P, 64), 2), dim3(64), 0, s, fl, fr, nl, nr, C, H * W, P);
+    hipLaunchKernelGGL(allpairs_corr_direct_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
+                       nl, nr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);
+  } else {
+    hipLaunchKernelGGL(allpairs_corr_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
+                       fl, fr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);
+  }
   return finish_launch("fsmi_allpairs_corr");
 }
 

@@ -31,12 +31,36 @@ __global__ __launch_bounds__(kT) void softmax_regression_kernel(const float* __r
   const long long b = p / HW;
   const int hw = static_cast<int>(p - b * HW);
   const float* src = logit + b * D * HW + hw;
+  // pass 1 from HBM with 8 loads in flight per lane; passes 2-3 re-read the column from L1/L2
+  constexpr int U = 8;
   float m = -INFINITY;
-  for (int d = 0; d < D; ++d) m = fmaxf(m, src[static_cast<size_t>(d) * HW]);
+  int d = 0;
+  for (; d + U <= D; d += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[static_cast<size_t>(d + u) * HW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) m = fmaxf(m, v[u]);
+  }
+  for (; d < D; ++d) m = fmaxf(m, src[static_cast<size_t>(d) * HW]);
   float s = 0.f;
-  for (int d = 0; d < D; ++d) s += expf(src[static_cast<size_t>(d) * HW] - m);
+  for (d = 0; d + U <= D; d += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[static_cast<size_t>(d + u) * HW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += expf(v[u] - m);
+  }
+  for (; d < D; ++d) s += expf(src[static_cast<size_t>(d) * HW] - m);
   float acc = 0.f;
-  for (int d = 0; d < D; ++d) acc += (expf(src[static_cast<size_t>(d) * HW] - m) / s) * static_cast<float>(d);
+  for (d = 0; d + U <= D; d += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[static_cast<size_t>(d + u) * HW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += (expf(v[u] - m) / s) * static_cast<float>(d + u);
+  }
+  for (; d < D; ++d) acc += (expf(src[static_cast<size_t>(d) * HW] - m) / s) * static_cast<float>(d);
   out[p] = acc;
 }
 

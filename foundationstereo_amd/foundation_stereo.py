@@ -198,8 +198,11 @@ class FoundationStereo(nn.Module):
             vol = self.corr_feature_att(vol, features_left[0])
             vol = self.cost_agg(vol, features_left)
             if init_disp is None:
-                logits = self.classifier(vol).squeeze(1)
-                init_disp = ops.softmax_regression(logits.float())
+                cl = self.classifier
+                head = cl[2]   # Conv3d(14, 1, 7, padding=3): direct gfx950 kernel (MIOpen: ~1 TFLOP/s here)
+                logits = ops.conv3d_direct(cl[1](cl[0](vol)).float(), head.weight.float(),
+                                           head.bias.float()).squeeze(1)
+                init_disp = ops.softmax_regression(logits)
             cnet_list = self.cnet(image1, vit_feat=vit_feat, num_layers=self.args.n_gru_layers)
             net_list = [torch.tanh(x[0]) for x in cnet_list]
             inp_list = [torch.relu(x[1]) for x in cnet_list]

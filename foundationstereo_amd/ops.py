@@ -83,30 +83,40 @@ def pointwise_proj(x: Tensor, wt: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
-def comb_volume_stem(fl: Tensor, fr: Tensor, A: Tensor, Bm: Tensor, Wg: Tensor, maxdisp: int) -> Tensor:
-    """Fused gwc + concat + corr_stem[0] (core/foundation_stereo.py:207-213,165) -> (B,Cs,D,H,W)."""
+def comb_volume_stem(fl: Tensor, fr: Tensor, A: Tensor, Bm: Tensor, Wg: Tensor, maxdisp: int,
+                     two_pass: bool = True) -> Tensor:
+    """Fused gwc + concat + corr_stem[0] (core/foundation_stereo.py:207-213,165) -> (B,Cs,D,H,W).
+
+    ``two_pass`` (default): gwc into a (B,G,D,H,W) scratch then one streaming
+    pass; otherwise a single LDS-staged kernel (no scratch)."""
     _check("comb_volume_stem", fl, fr, A, Bm, Wg)
     B, C, H, W = fl.shape
     Cs, G = Wg.shape
     assert C % G == 0, f"C:{C}, num_groups:{G}"
     fl, fr, A, Bm, Wg = _c(fl), _c(fr), _c(A), _c(Bm), _c(Wg)
     out = torch.empty((B, Cs, maxdisp, H, W), device=fl.device, dtype=torch.float32)
-    _lib.check(_lib.load().fsmi_comb_volume_stem(_p(fl), _p(fr), _p(A), _p(Bm), _p(Wg), _p(out), B, C, G, Cs,
+    ws = torch.empty((B, G, maxdisp, H, W), device=fl.device, dtype=torch.float32) if two_pass else None
+    _lib.check(_lib.load().fsmi_comb_volume_stem(_p(fl), _p(fr), _p(A), _p(Bm), _p(Wg),
+                                                 _p(ws) if ws is not None else None, _p(out), B, C, G, Cs,
                                                  maxdisp, H, W, _stream(fl)), "comb_volume_stem")
     return out
 
 
 # ---------------------------------------------------------------- geometry
 
-def allpairs_corr(fl: Tensor, fr: Tensor, num_levels: int) -> List[Tensor]:
-    """core/geometry.py:24-40,68-77 -> [(B,H,W,W_i)] with W_i = W >> i."""
+def allpairs_corr(fl: Tensor, fr: Tensor, num_levels: int, two_pass: bool = True) -> List[Tensor]:
+    """core/geometry.py:24-40,68-77 -> [(B,H,W,W_i)] with W_i = W >> i.
+
+    ``two_pass`` (default): normalise into a scratch, then the barrier-free MFMA
+    pass; otherwise one LDS-staged kernel."""
     _check("allpairs_corr", fl, fr)
     B, C, H, W = fl.shape
     fl, fr = _c(fl), _c(fr)
     levels = [torch.empty((B, H, W, W >> i), device=fl.device, dtype=torch.float32) for i in range(num_levels)]
+    ws = torch.empty((2, B, C, H, W), device=fl.device, dtype=torch.float32) if two_pass else None
     pp, keep = _lib.ptr_array([_p(t) for t in levels])
-    _lib.check(_lib.load().fsmi_allpairs_corr(_p(fl), _p(fr), pp, num_levels, B, C, H, W, _stream(fl)),
-               "allpairs_corr")
+    _lib.check(_lib.load().fsmi_allpairs_corr(_p(fl), _p(fr), pp, num_levels, B, C, H, W,
+                                              _p(ws) if ws is not None else None, _stream(fl)), "allpairs_corr")
     del keep
     return levels
 
@@ -233,6 +243,19 @@ def gru_blend(zr_s: Tensor, zr_l: Tensor, q_s: Tensor, q_l: Tensor, h: Tensor, a
     out = torch.empty_like(h)
     _lib.check(_lib.load().fsmi_gru_blend(_p(zr_s), _p(zr_l), _p(q_s), _p(q_l), _p(h), _p(att), _p(out), B, Hd,
                                           H, W, _stream(h)), "gru_blend")
+    return out
+
+
+def conv3d_direct(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
+    """Stride-1, zero-padded (KS//2) 3D conv for Cout == 1 (the classifier head, core/foundation_stereo.py:175)."""
+    _check("conv3d_direct", x, w, *([bias] if bias is not None else []))
+    B, Cin, D, H, W = x.shape
+    Cout, Cw, KS = w.shape[0], w.shape[1], w.shape[2]
+    assert Cw == Cin and tuple(w.shape[2:]) == (KS, KS, KS)
+    x, w = _c(x), _c(w)
+    out = torch.empty((B, Cout, D, H, W), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_conv3d_direct(_p(x), _p(w), _p(bias) if bias is not None else None, _p(out), B, Cin,
+                                              Cout, KS, D, H, W, _stream(x)), "conv3d_direct")
     return out
 
 

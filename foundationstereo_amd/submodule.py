@@ -376,7 +376,9 @@ class ChannelAttentionEnhancement(nn.Module):
         self.sigmoid = nn.Sigmoid()
 
     def forward(self, x):
-        return self.sigmoid(self.fc(self.avg_pool(x)) + self.fc(self.max_pool(x)))
+        # global pools as plain reductions: identical values to AdaptiveAvg/MaxPool2d(1), and
+        # the ROCm adaptive-max kernel takes ~0.7 ms on a (1,128,120,160) map
+        return self.sigmoid(self.fc(x.mean((2, 3), keepdim=True)) + self.fc(x.amax((2, 3), keepdim=True)))
 
 
 class SpatialAttentionExtractor(nn.Module):

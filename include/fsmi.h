@@ -53,9 +53,11 @@ int fsmi_concat_volume(const float* pl, const float* pr, float* out,
  *   out[b,o,d,h,w] = A[b,o,h,w] + [w>=d] Bm[b,o,h,w-d] + sum_g Wg[o,g] gwc[b,g,d,h,w]
  * where A, Bm: (B,Cs,H,W) are the proj_cmb features already multiplied by the
  * concat columns of the stem weight (A also carries the stem bias), and
- * Wg: (Cs,G) the gwc columns.  out: (B,Cs,D,H,W). */
+ * Wg: (Cs,G) the gwc columns.  out: (B,Cs,D,H,W).  gwc_ws: optional
+ * (B,G,D,H,W) scratch; with it the build runs as two streaming passes (gwc
+ * tile kernel, then the stem stream), without it as one LDS-staged kernel. */
 int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, const float* Bm,
-                          const float* Wg, float* out,
+                          const float* Wg, float* gwc_ws, float* out,
                           int B, int C, int G, int Cs, int D, int H, int W, void* stream);
 
 /* pointwise 2-output projection used to form A / Bm above:
@@ -67,9 +69,11 @@ int fsmi_pointwise_proj(const float* x, const float* Wt, const float* bias, floa
  * replaces Combined_Geo_Encoding_Volume.corr + its avg-pool pyramid,
  * core/geometry.py:24-40,68-77.  fl, fr: (B,C,H,W).  levels[i]: (B,H,W,W>>i')
  * with W_i = floor(W_{i-1}/2); level 0 is the full (B,H,W1,W2) correlation of
- * the channel-L2-normalised features. */
+ * the channel-L2-normalised features.  ws: optional 2*B*C*H*W-float scratch;
+ * with it the features are normalised once and the MFMA pass reads them
+ * straight from L2, without it one LDS-staged kernel normalises per block. */
 int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, int num_levels,
-                       int B, int C, int H, int W, void* stream);
+                       int B, int C, int H, int W, float* ws, void* stream);
 
 /* ---- a5: filtered-volume pyramid over D ---------------------------------
  * replaces core/geometry.py:29,34-36 without the permute copy.  vol:
@@ -125,6 +129,14 @@ int fsmi_gru_blend(const float* zr_s, const float* zr_l, const float* q_s, const
                    const float* h, const float* att, float* hout,
                    int B, int Hd, int H, int W, void* stream);
 
+/* ---- a3: few-output-channel direct 3D convolution ------------------------
+ * replaces the classifier's final nn.Conv3d(14, 1, kernel_size=7, padding=3)
+ * (core/foundation_stereo.py:175): x (B,Cin,D,H,W), w (Cout,Cin,KS,KS,KS),
+ * bias (Cout) or NULL -> out (B,Cout,D,H,W); stride 1, zero padding KS/2.
+ * Supported (KS, Cout): (7,1), (3,1). */
+int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float* out,
+                       int B, int Cin, int Cout, int KS, int D, int H, int W, void* stream);
+
 /* ---- live kernel timing (bench.py roofline) -----------------------------
  * When enabled, every launch of the kernels below is bracketed by a pair of
  * hipEvents recorded on the launch stream (skipped while the stream is being
@@ -133,7 +145,7 @@ int fsmi_gru_blend(const float* zr_s, const float* zr_l, const float* q_s, const
 enum {
   FSMI_K_GWC = 0, FSMI_K_CONCAT, FSMI_K_COMB, FSMI_K_PROJ, FSMI_K_CORR, FSMI_K_VOLPYR,
   FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
-  FSMI_K_COUNT
+  FSMI_K_CONV3D, FSMI_K_COUNT
 };
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);

@@ -85,10 +85,25 @@ def test_comb_volume_stem_vs_oracle(ops_mod, vit, W):
                           oracle.build_concat_volume(oracle.stereo_oracle._conv(P, "proj_cmb", t(fl)),
                                                      oracle.stereo_oracle._conv(P, "proj_cmb", t(fr)), D)], 1)
         ref = oracle.stereo_oracle._conv(P, "corr_stem.0", comb)
+        wg, wa, ba, wb, bb = m._stem_weights()
+        A, Bm = ops_mod.pointwise_proj(g(fl), wa, ba), ops_mod.pointwise_proj(g(fr), wb, bb)
+        one_pass = ops_mod.comb_volume_stem(g(fl), g(fr), A, Bm, wg, D, two_pass=False)
         m.fused_volume = False
         unfused = m.build_stem_volume(g(fl), g(fr))
     close(out, ref, atol=2e-5)
+    close(one_pass, ref, atol=2e-5)
     close(unfused, ref, atol=2e-5)
+
+
+@pytest.mark.parametrize("KS,shape", [(7, (1, 14, 12, 16, 40)), (7, (2, 5, 5, 9, 33)), (3, (1, 14, 8, 8, 64))])
+def test_conv3d_direct_vs_torch(ops_mod, KS, shape):
+    """Classifier head Conv3d(Cin, 1, KS, padding=KS//2) vs the fp32 torch CPU conv (ragged tiles included)."""
+    x = synth.normal(81, shape)
+    w = synth.normal(82, (1, shape[1], KS, KS, KS), 0.05)
+    b = synth.normal(83, (1,), 0.1)
+    ref = torch.nn.functional.conv3d(t(x).double(), t(w).double(), t(b).double(), padding=KS // 2)
+    # fp32 sums of Cin*KS^3 (up to 4802) products vs an fp64 reference
+    close(ops_mod.conv3d_direct(g(x), g(w), g(b)), ref, atol=2e-5, rtol=1e-5)
 
 
 # ------------------------------------------------------------------ a4 / a9
@@ -128,9 +143,11 @@ def test_geo_encoding_golden(ops_mod, gold, L):
 def test_allpairs_corr_vs_oracle(ops_mod, C, H, W):
     f1, f2 = synth.normal(41, (2, C, H, W)), synth.normal(42, (2, C, H, W))
     lv = ops_mod.allpairs_corr(g(f1), g(f2), 4)
+    lv1 = ops_mod.allpairs_corr(g(f1), g(f2), 4, two_pass=False)
     ref = oracle.allpairs_corr(t(f1), t(f2))
     for i in range(4):
         close(lv[i], ref, atol=3e-6)
+        close(lv1[i], ref, atol=3e-6)
         ref = oracle.stereo_oracle._pool_last(ref)
 
 
