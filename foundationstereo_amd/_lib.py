@@ -36,13 +36,19 @@ SIGNATURES = {
     "fsmi_gru_reset": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_gru_blend": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_conv3d_direct": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_conv2d": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I,
+                    _I, _I, _I, _I, _F, _I, _P],
+    "fsmi_conv2d_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _P, _P, _I, _P, _I, _I,
+                       _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+    "fsmi_conv2d_halo_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _P, _P, _I, _P, _I,
+                            _I, _I, _I, _I, _I, _I, _I, _F, _I, _I, _P, ctypes.c_longlong, _P],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
-           "gru_reset", "gru_blend", "conv3d"]
+           "gru_reset", "gru_blend", "conv3d", "conv2d"]
 
 _lib = None
 

@@ -259,6 +259,131 @@ def conv3d_direct(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
+def pack_conv_weight(*weights: Tensor) -> Tensor:
+    """Pack conv weights (Cout_i, Cin, KH, KW), stacked along Cout, into the
+    ``fsmi_conv2d`` layout [KH*KW*Cin][roundup(Cout,4)] (k = (kh*KW + kw)*Cin + ci)."""
+    w = torch.cat([x.detach().float() for x in weights], 0)
+    Cout, Cin, KH, KW = w.shape
+    coutp = (Cout + 3) // 4 * 4
+    pk = torch.zeros((KH * KW * Cin, coutp), device=w.device, dtype=torch.float32)
+    pk[:, :Cout] = w.permute(2, 3, 1, 0).reshape(KH * KW * Cin, Cout)
+    return pk
+
+
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+
+
+class PackedConv:
+    """Conv weights packed once for the implicit-GEMM kernels.
+
+    ``mode`` "f32": fp32 MFMA (``fsmi_conv2d``); "x3": split-precision fp16
+    MFMA (``fsmi_conv2d_x3``: hi/lo halves of the weights pre-scaled by 2^wexp);
+    "halo": the same packed halves run by the halo-tiled ``fsmi_conv2d_halo_x3``
+    (square 1x1 / 3x3 only).
+    Several weight tensors stacked along Cout form one conv (e.g. convz|convr).
+    """
+
+    def __init__(self, *weights: Tensor, mode: str = "x3"):
+        w = torch.cat([x.detach().float() for x in weights], 0)
+        self.cout, self.cin, self.k, kw = w.shape
+        assert self.k == kw
+        self.mode = mode
+        assert mode in ("f32", "x3", "halo"), mode
+        assert mode != "halo" or self.k in (1, 3), "halo conv: 1x1 or 3x3 only"
+        if mode == "f32":
+            self.wpk = pack_conv_weight(w)
+            return
+        import math
+        amax = float(w.abs().max())
+        self.wexp = 0 if amax == 0 else -int(math.floor(math.log2(amax)))   # max |w| * 2^wexp in [1, 2)
+        cinp = (self.cin + 31) // 32 * 32
+        coutp = (self.cout + 31) // 32 * 32
+        ws = torch.zeros((coutp, cinp, self.k, self.k), device=w.device, dtype=torch.float32)
+        ws[:self.cout, :self.cin] = w * (2.0 ** self.wexp)
+        # [tap][cin chunk][cout][32]
+        ws = ws.permute(2, 3, 1, 0).reshape(self.k * self.k, cinp // 32, 32, coutp).permute(0, 1, 3, 2).contiguous()
+        hi = ws.half()
+        lo = (ws - hi.float()).half()
+        self.whi, self.wlo = hi.contiguous(), lo.contiguous()
+
+
+def _segments(segs):
+    import ctypes
+    norm = []
+    for s in segs:
+        t, c0, n = (s, 0, s.shape[1]) if isinstance(s, torch.Tensor) else s
+        norm.append((t, c0, n))
+    t0 = norm[0][0]
+    B, _, H, W = t0.shape
+    HW = H * W
+    for t, c0, n in norm:
+        assert t.is_contiguous() and t.shape[0] == B and t.shape[2:] == (H, W) and c0 + n <= t.shape[1], \
+            "conv2d: segment shape mismatch"
+    nseg = len(norm)
+    ptrs = (ctypes.c_void_p * nseg)(*[t.data_ptr() + 4 * c0 * HW for t, c0, _ in norm])
+    chs = (ctypes.c_int * nseg)(*[n for _, _, n in norm])
+    tots = (ctypes.c_int * nseg)(*[t.shape[1] for t, _, _ in norm])
+    return norm, (ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), chs, tots, ptrs), sum(n for _, _, n in norm)
+
+
+_SPLIT_WS = {}
+
+
+def _split_workspace(dev, stream, floats: int):
+    """Split-K partial-sum buffer, one per (device, stream); reuse is stream-ordered."""
+    key = (dev, stream)
+    ws = _SPLIT_WS.get(key)
+    if ws is None or ws.numel() < floats:
+        ws = torch.empty(max(floats, 1 << 22), device=dev, dtype=torch.float32)
+        _SPLIT_WS[key] = ws
+    return ws
+
+
+def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=None, alpha: float = 1.0,
+           gamma: Tensor = None, res: Tensor = None, out: Tensor = None, co0: int = 0, cfg: int = -1,
+           nsplit: int = -1) -> Tensor:
+    """Implicit-GEMM conv (stride 1, 'same' zero padding) on MFMA.
+
+    ``segs``: list of NCHW tensors or ``(tensor, c_start, c_count)`` channel slices,
+    concatenated along C without a copy.  ``pk``: a ``PackedConv`` (or a raw
+    ``pack_conv_weight`` tensor with ``cout``/``k`` given: fp32 path).  Writes
+    ``out[:, co0:co0+cout]`` (allocated as (B, cout, H, W) when None) =
+    ``res + gamma * alpha * act(conv + bias)``."""
+    if isinstance(pk, torch.Tensor):
+        raw = pk
+        pk = PackedConv.__new__(PackedConv)
+        pk.mode, pk.wpk, pk.cout, pk.k = "f32", raw, cout, k
+        pk.cin = raw.shape[0] // (k * k)
+    norm, (pp, chs, tots, keep), cin = _segments(segs)
+    t0 = norm[0][0]
+    B, _, H, W = t0.shape
+    extra = [x for x in (bias, gamma, res) if x is not None]
+    _check("conv2d", *[t for t, _, _ in norm], *extra)
+    assert cin == pk.cin, f"conv2d: {cin} input channels for a conv packed with {pk.cin}"
+    if out is None:
+        out = torch.empty((B, pk.cout, H, W), device=t0.device, dtype=torch.float32)
+    assert out.is_contiguous() and out.shape[0] == B and out.shape[2:] == (H, W)
+    if res is not None:
+        assert res.is_contiguous() and res.shape[2:] == (H, W)
+    common = (_p(bias) if bias is not None else None, _p(gamma) if gamma is not None else None,
+              _p(res) if res is not None else None, res.shape[1] if res is not None else 0,
+              _p(out), out.shape[1], co0, B, pk.cout, pk.k, pk.k, H, W, ACT[act], float(alpha), cfg, _stream(t0))
+    lib = _lib.load()
+    if pk.mode == "f32":
+        _lib.check(lib.fsmi_conv2d(pp, chs, tots, len(norm), _p(pk.wpk), *common), "conv2d")
+    elif pk.mode == "x3":
+        _lib.check(lib.fsmi_conv2d_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, *common),
+                   "conv2d_x3")
+    else:
+        # auto split-K is capped at 8; the workspace covers that for this output
+        ws = _split_workspace(t0.device, common[-1], 8 * B * pk.cout * H * W)
+        hc = common[:9] + (pk.k,) + common[11:-1] + (nsplit, _p(ws), ws.numel(), common[-1])
+        _lib.check(lib.fsmi_conv2d_halo_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, *hc),
+                   "conv2d_halo_x3")
+    del keep
+    return out
+
+
 # ---------------------------------------------------------------- timing
 
 def timer_enable(on: bool = True):

@@ -137,6 +137,47 @@ int fsmi_gru_blend(const float* zr_s, const float* zr_l, const float* q_s, const
 int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float* out,
                        int B, int Cin, int Cout, int KS, int D, int H, int W, void* stream);
 
+/* ---- a7: implicit-GEMM 2D convolution (fp32 MFMA) ------------------------
+ * replaces the nn.Conv2d / nn.Linear stacks of the refinement loop
+ * (core/update.py:20-159: motion encoder, SelectiveConvGRU convs, DispHead,
+ * mask head) plus the elementwise passes that follow them.
+ * Input: nseg NCHW channel segments concatenated along C (zero-copy cat):
+ *   segment i = seg_ch[i] channels starting at seg_ptr[i] inside a tensor with
+ *   seg_ctot[i] channels per image (batch stride seg_ctot[i]*H*W).
+ * wpk: weights packed [KH*KW*Cin][roundup(Cout,4)] (k = (kh*KW+kw)*Cin + ci), zero padded.
+ * out[b, co0+co] (tensor with out_ctot channels) =
+ *   res[b,co] + gamma[co] * alpha * act(conv + bias[co]);  act 0 none, 1 ReLU, 2 GELU(erf);
+ *   bias/gamma/res may be NULL (res has res_ctot channels per image).
+ * KHxKW in {1x1, 3x3, 7x7}, stride 1, zero padding K/2.  cfg: tile config or -1 (auto). */
+int fsmi_conv2d(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
+                const float* wpk, const float* bias, const float* gamma, const float* res, int res_ctot,
+                float* out, int out_ctot, int co0, int B, int Cout, int KH, int KW, int H, int W, int act,
+                float alpha, int cfg, void* stream);
+
+/* Same convolution with split-precision operands on the fp16 MFMA ("3 x fp16"):
+ * x = hi + lo (two fp16), product = hi*hi + hi*lo + lo*hi accumulated in fp32
+ * (~22-bit operands, ~5x the fp32-MFMA rate).  whi/wlo: _Float16 weights packed
+ * [KH*KW][Cin32/32][Cout32][32] (Cin32/Cout32 = Cin/Cout rounded up to 32, zero
+ * padded), pre-multiplied by 2^wexp; the epilogue multiplies by 2^-wexp. */
+int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
+                   const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
+                   const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
+                   int KH, int KW, int H, int W, int act, float alpha, int cfg, void* stream);
+
+/* Halo-tiled variant of fsmi_conv2d_x3 (same weights, same epilogue) for
+ * square KS in {1, 3}: a block stages a (rows+2)x34 input halo once per
+ * 32-channel chunk and runs all taps from LDS.  Inner segments must hold a
+ * multiple of 8 channels.  cfg 0: 64 couts x 8x32 px; 1: 128 couts x 4x32 px.
+ * nsplit: split-K over 32-channel chunks (<0: auto, sized to fill the chip);
+ * partial sums go to ws (nsplit*B*Cout*H*W floats, ws_floats available) and
+ * a second kernel sums them in split order (deterministic) and applies the
+ * epilogue.  ws may be NULL when nsplit is 0/1 (or auto: then no split). */
+int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
+                        const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
+                        const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
+                        int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
+                        long long ws_floats, void* stream);
+
 /* ---- live kernel timing (bench.py roofline) -----------------------------
  * When enabled, every launch of the kernels below is bracketed by a pair of
  * hipEvents recorded on the launch stream (skipped while the stream is being
@@ -145,7 +186,7 @@ int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float*
 enum {
   FSMI_K_GWC = 0, FSMI_K_CONCAT, FSMI_K_COMB, FSMI_K_PROJ, FSMI_K_CORR, FSMI_K_VOLPYR,
   FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
-  FSMI_K_CONV3D, FSMI_K_COUNT
+  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_COUNT
 };
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);

@@ -106,6 +106,63 @@ def test_conv3d_direct_vs_torch(ops_mod, KS, shape):
     close(ops_mod.conv3d_direct(g(x), g(w), g(b)), ref, atol=2e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("mode", ["f32", "x3"])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (7, 64, "relu"), (3, 128, None)])
+def test_conv2d_mfma_vs_torch(ops_mod, mode, cfg, k, cout, act):
+    """Implicit-GEMM conv (fp32 MFMA and split-precision 3 x fp16 MFMA): 2 input segments (one a
+    channel slice), ragged pixels/couts, output slice, every epilogue term, all tile configs; vs an
+    fp64 torch reference.  Tolerance 2e-5 abs + 1e-5 rel for both (x3 operands carry 22 bits)."""
+    import torch.nn.functional as F
+    B, H, W = 2, 9, 13
+    a_ = synth.normal(91, (B, 5, H, W))
+    c_ = synth.normal(92, (B, 12, H, W))
+    cin = 5 + 7 if k != 7 else 1
+    w = synth.normal(93, (cout, cin, k, k), 0.2)
+    bias = synth.normal(94, (cout,), 0.1)
+    gamma = synth.uniform(95, (cout,), 0.5, 1.5)
+    res = synth.normal(96, (B, cout, H, W))
+    if k == 7:
+        segs, x = [g(a_[:, :1].copy())], t(a_[:, :1])
+    else:
+        segs, x = [g(a_), (g(c_), 3, 7)], torch.cat([t(a_), t(c_[:, 3:10])], 1)
+    out = torch.zeros(B, cout + 3, H, W, device=DEV)
+    ops_mod.conv2d(segs, ops_mod.PackedConv(g(w), mode=mode), bias=g(bias), act=act, alpha=0.75, gamma=g(gamma),
+                   res=g(res), out=out, co0=2, cfg=cfg)
+    y = F.conv2d(x.double(), t(w).double(), t(bias).double(), padding=k // 2)
+    y = {"relu": F.relu, "gelu": F.gelu, None: lambda v: v}[act](y)
+    ref = t(res).double() + t(gamma).double().view(1, -1, 1, 1) * 0.75 * y
+    close(out[:, 2:2 + cout], ref, atol=2e-5, rtol=1e-5)
+    assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
+
+
+@pytest.mark.parametrize("nsplit", [1, 2])
+@pytest.mark.parametrize("cfg", [-1, 0, 1])
+@pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (3, 136, None), (1, 129, "relu")])
+def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit):
+    """Halo-tiled split-precision conv: 2 segments (16 channels + a 29-channel slice -> 2 channel
+    chunks, ragged last chunk), ragged row/column tiles (19x45), ragged couts, output slice, every
+    epilogue term, with and without split-K; vs fp64 torch.  Same 2e-5 abs + 1e-5 rel tolerance as
+    the im2col kernels."""
+    import torch.nn.functional as F
+    B, H, W = 2, 19, 45
+    a_ = synth.normal(191, (B, 16, H, W))
+    c_ = synth.normal(192, (B, 40, H, W))
+    w = synth.normal(193, (cout, 45, k, k), 0.2)
+    bias = synth.normal(194, (cout,), 0.1)
+    gamma = synth.uniform(195, (cout,), 0.5, 1.5)
+    res = synth.normal(196, (B, cout, H, W))
+    segs, x = [g(a_), (g(c_), 5, 29)], torch.cat([t(a_), t(c_[:, 5:34])], 1)
+    out = torch.zeros(B, cout + 3, H, W, device=DEV)
+    ops_mod.conv2d(segs, ops_mod.PackedConv(g(w), mode="halo"), bias=g(bias), act=act, alpha=0.75,
+                   gamma=g(gamma), res=g(res), out=out, co0=2, cfg=cfg, nsplit=nsplit)
+    y = F.conv2d(x.double(), t(w).double(), t(bias).double(), padding=k // 2)
+    y = {"relu": F.relu, "gelu": F.gelu, None: lambda v: v}[act](y)
+    ref = t(res).double() + t(gamma).double().view(1, -1, 1, 1) * 0.75 * y
+    close(out[:, 2:2 + cout], ref, atol=2e-5, rtol=1e-5)
+    assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
+
+
 # ------------------------------------------------------------------ a4 / a9
 
 def test_regression_golden(ops_mod, gold):
