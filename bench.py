@@ -104,7 +104,11 @@ def main():
                     help="MIOpen Find (exhaustive, slow first call) instead of immediate-mode heuristics")
     ap.add_argument("--mixed-precision", action="store_true",
                     help="fp16 autocast for the dense convs (the reference GPU default); volumes/lookup stay fp32")
+    ap.add_argument("--conv-engine", default="fsmi", choices=["fsmi", "miopen"],
+                    help="refinement-loop convs: halo-tiled split-precision MFMA kernels or MIOpen (A/B)")
     a = ap.parse_args()
+    from foundationstereo_amd import update as fupdate
+    fupdate.CONV_ENGINE = a.conv_engine
 
     rank, local, world = fdist.init_from_env("nccl")
     device = torch.device("cuda", local)
@@ -202,7 +206,7 @@ def main():
         "config": {"workload": f"{a.config}: {W}x{H}, max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",
                    "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,
-                   "corr_levels": L, "parallelism": f"dp{world}"},
+                   "corr_levels": L, "conv_engine": a.conv_engine, "parallelism": f"dp{world}"},
         "roofline": {"kernel": "geo_lookup", "bound": "hbm", "achieved": lk_bytes / lk_avg / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
                      "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,

@@ -1,12 +1,17 @@
 """Drop-in for ``core/update.py``: the selective ConvGRU refinement block.
 
-Convolutions run on MIOpen (``torch.nn``); everything between them that the
-reference does as separate elementwise passes -- sigmoid of the z/r gates,
-``r*h``, the ``cat([r*h, x])`` copy, ``tanh``, the ``(1-z)h + zq`` update and
-the ``small*att + large*(1-att)`` selection -- is two fused gfx950 kernels per
-SelectiveConvGRU (``ops.gru_reset``, ``ops.gru_blend``).  ``convz`` and
-``convr`` of each GRU share their input, so they run as ONE convolution with
-the two weight tensors stacked (half the passes over ``hx``).
+Every 1x1 / 3x3 convolution of the loop (motion encoder, SelectiveConvGRU,
+DispHead incl. the EdgeNeXt MLPs, mask head) runs on the halo-tiled
+split-precision MFMA kernel (``ops.conv2d``, ``fsmi_conv2d_halo_x3``) with
+the reference's cats done as zero-copy input segments and bias / ReLU / GELU /
+layer-scale / residual / 0.25-scale fused into the epilogue.  Weights are
+packed once per (module, weight version).  The gates between the convs --
+sigmoid of z/r, ``r*h``, ``cat([r*h, x])``, ``tanh``, ``(1-z)h + zq`` and the
+``small*att + large*(1-att)`` selection -- are two fused kernels per
+SelectiveConvGRU (``ops.gru_reset``, ``ops.gru_blend``); ``convz`` and
+``convr`` run as ONE conv with stacked weights.  Only the two 7x7 convs
+(``convd1``, the depthwise ``dwconv``) stay on MIOpen, as does everything
+under autocast (``CONV_ENGINE = "miopen"`` forces the MIOpen path for A/B).
 """
 from __future__ import annotations
 
@@ -16,6 +21,36 @@ import torch.nn.functional as F
 
 from . import ops
 from .submodule import EdgeNextConvEncoder
+
+CONV_ENGINE = "fsmi"
+
+
+def _fast(x) -> bool:
+    return (CONV_ENGINE == "fsmi" and x.is_cuda and x.dtype == torch.float32
+            and not torch.is_autocast_enabled() and not torch.is_grad_enabled())
+
+
+def _packed(*mods):
+    """Halo-kernel weights of one Conv2d/Linear (or several stacked along Cout),
+    cached on the first module and rebuilt when any weight/bias changes."""
+    key = tuple((id(m), m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version)
+                for m in mods)
+    hit = mods[0].__dict__.get("_fsmi_pack")
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            ws = [m.weight if m.weight.dim() == 4 else m.weight[:, :, None, None] for m in mods]
+            pk = ops.PackedConv(*ws, mode="halo")
+            bias = torch.cat([m.bias.detach().float() for m in mods]).contiguous()
+        hit = (key, pk, bias)
+        mods[0].__dict__["_fsmi_pack"] = hit
+    return hit[1], hit[2]
+
+
+def _conv(mods, segs, act=None, **kw):
+    mods = mods if isinstance(mods, tuple) else (mods,)
+    pk, bias = _packed(*mods)
+    return ops.conv2d(segs, pk, bias=bias, act=act, **kw)
+
 
 __all__ = ["DispHead", "ConvGRU", "BasicMotionEncoder", "pool2x", "pool4x", "interp", "RaftConvGRU",
            "SelectiveConvGRU", "BasicSelectiveMultiUpdateBlock"]
@@ -33,7 +68,14 @@ class DispHead(nn.Module):
             nn.Conv2d(input_dim, output_dim, 3, padding=1))
 
     def forward(self, x):
-        return self.conv(x)
+        if not _fast(x):
+            return self.conv(x)
+        y = _conv(self.conv[0], [x], "relu")
+        for enc in (self.conv[2], self.conv[3]):
+            d = enc.dwconv(y)                                   # depthwise 7x7 (MIOpen); norm=None
+            e = _conv(enc.pwconv1, [d], "gelu")
+            y = _conv(enc.pwconv2, [e], gamma=enc.gamma, res=y)  # x + gamma * pw2(gelu(pw1(.)))
+        return _conv(self.conv[4], [y])
 
 
 class ConvGRU(nn.Module):
@@ -68,7 +110,19 @@ class BasicMotionEncoder(nn.Module):
         self.convd2 = nn.Conv2d(64, 64, 3, padding=1)
         self.conv = nn.Conv2d(64 + 256, 128 - 1, 3, padding=1)
 
+    def encode_into(self, disp, corr, out):
+        """Writes cat([relu(conv(...)), disp]) into ``out`` (B, 128, H, W) without the cat copy."""
+        c = _conv(self.convc2, [_conv(self.convc1, [corr], "relu")], "relu")
+        d = F.relu_(self.convd1(disp))                          # 7x7, 1 -> 64 (MIOpen)
+        d = _conv(self.convd2, [d], "relu")
+        _conv(self.conv, [c, d], "relu", out=out, co0=0)
+        out[:, self.conv.out_channels:].copy_(disp)
+        return out
+
     def forward(self, disp, corr):
+        if _fast(corr):
+            B, _, H, W = corr.shape
+            return self.encode_into(disp, corr, corr.new_empty(B, self.conv.out_channels + 1, H, W))
         cor = F.relu(self.convc2(F.relu(self.convc1(corr))))
         dsp = F.relu(self.convd2(F.relu(self.convd1(disp))))
         out = F.relu(self.conv(torch.cat([cor, dsp], dim=1)))
@@ -114,10 +168,13 @@ class RaftConvGRU(nn.Module):
         w, b = _stacked_zr(self, self._zr_cache)
         return F.conv2d(hx, w, b, padding=self.convz.padding)
 
+    def zr_fast(self, hx):
+        return _conv((self.convz, self.convr), [hx])
+
     def forward(self, h, x, hx):
-        zr = self.zr(hx)
+        zr = self.zr_fast(hx) if _fast(hx) else self.zr(hx)
         qin, _ = ops.gru_reset(zr, zr, h, x)
-        q = self.convq(qin)
+        q = _conv(self.convq, [qin]) if _fast(qin) else self.convq(qin)
         ones = torch.ones_like(h[:, :1])
         return ops.gru_blend(zr, zr, q, q, h, ones)
 
@@ -134,6 +191,15 @@ class SelectiveConvGRU(nn.Module):
         self.large_gru = RaftConvGRU(hidden_dim, input_dim, large_kernel_size)
 
     def forward(self, att, h, *x):
+        if _fast(h):
+            xc = _conv(self.conv0[0], list(x), "relu")              # cat(x) as input segments
+            hx = _conv(self.conv1[0], [xc, h], "relu")
+            zr_s = self.small_gru.zr_fast(hx)
+            zr_l = self.large_gru.zr_fast(hx)
+            qs_in, ql_in = ops.gru_reset(zr_s, zr_l, h, xc)
+            q_s = _conv(self.small_gru.convq, [qs_in])
+            q_l = _conv(self.large_gru.convq, [ql_in])
+            return ops.gru_blend(zr_s, zr_l, q_s, q_l, h, att.float())
         x = torch.cat(x, dim=1) if len(x) > 1 else x[0]
         x = self.conv0(x)
         hx = self.conv1(torch.cat([x, h], dim=1))
@@ -165,6 +231,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                                   nn.Conv2d(64, 32, 3, padding=1), nn.ReLU(inplace=True))
 
     def forward(self, net, inp, corr, disp, att):
+        if _fast(corr):
+            return self._forward_fast(net, inp, corr, disp, att)
         n = self.args.n_gru_layers
         if n == 3:
             net[2] = self.gru16(att[2], net[2], inp[2], pool2x(net[1]))
@@ -178,4 +246,22 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             net[0] = self.gru04(att[0], net[0], motion, interp(net[1], net[0]))
         delta_disp = self.disp_head(net[0])
         mask = .25 * self.mask(net[0])
+        return net, mask, delta_disp
+
+    def _forward_fast(self, net, inp, corr, disp, att):
+        n = self.args.n_gru_layers
+        if n == 3:
+            net[2] = self.gru16(att[2], net[2], inp[2], pool2x(net[1]))
+        if n >= 2:
+            if n > 2:
+                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]), interp(net[2], net[1]))
+            else:
+                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]))
+        B, _, H, W = corr.shape
+        enc = self.encoder.encode_into(disp, corr, corr.new_empty(B, self.encoder.conv.out_channels + 1, H, W))
+        # motion = cat([inp[0], enc]) stays two segments of gru04.conv0's input
+        if n > 1:
+            net[0] = self.gru04(att[0], net[0], inp[0], enc, interp(net[1], net[0]))
+        delta_disp = self.disp_head(net[0])
+        mask = _conv(self.mask[2], [_conv(self.mask[0], [net[0]], "relu")], "relu", alpha=0.25)
         return net, mask, delta_disp
