@@ -42,13 +42,15 @@ SIGNATURES = {
                        _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
     "fsmi_conv2d_halo_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _P, _P, _I, _P, _I,
                             _I, _I, _I, _I, _I, _I, _I, _F, _I, _I, _P, ctypes.c_longlong, _P],
+    "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
-           "gru_reset", "gru_blend", "conv3d", "conv2d"]
+           "gru_reset", "gru_blend", "conv3d", "conv2d", "dwconv", "resize"]
 
 _lib = None
 

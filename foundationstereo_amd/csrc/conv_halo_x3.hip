@@ -344,9 +344,12 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
   const int nck = a.CinP / HKC;
   const long long per_split = static_cast<long long>(B) * Cout * H * W;
   if (nsplit < 0) {
+    // measured on the cfg2 loop layers (tools/conv_bench.py --nsplit): 3x3 layers are best
+    // near ~1200 blocks (~2.3 rounds of the 512 resident slots), 1x1 layers -- a quarter of
+    // the MFMA work per chunk, so the extra reduce pass weighs more -- near ~400
     const int base = a.npix * a.nco;
-    nsplit = base >= 512 ? 1 : (512 + base - 1) / base;
-    nsplit = min(nsplit, nck / 2 > 0 ? nck / 2 : 1);      // keep >= 2 chunks per split
+    nsplit = max(1, (KS == 3 ? 1200 : 400) / base);
+    nsplit = min(nsplit, min(8, nck / 2 > 0 ? nck / 2 : 1));      // keep >= 2 chunks per split
     if (!ws) nsplit = 1;
     else if (per_split * nsplit > ws_floats) nsplit = static_cast<int>(max(1LL, ws_floats / per_split));
   }

@@ -1,0 +1,114 @@
+// Refinement-loop auxiliaries that MIOpen / ATen run poorly at these shapes:
+//  * depthwise KxK conv (EdgeNeXt dwconv of DispHead, core/submodule.py:565-591):
+//    MIOpen routes it through NCHW->NHWC transposes and a grouped CK kernel
+//    (~105 us at 128x120x160); here it is one LDS-tiled pass (HBM-bound: one
+//    read + one write of the plane);
+//  * bilinear resize with align_corners=True (interp(), core/update.py:80).
+#include "fsmi_common.h"
+
+namespace fsmi {
+namespace {
+
+constexpr int DW_TR = 16, DW_TC = 64;   // output tile per block (rows x cols), 4 rows per thread
+
+template <int KS>
+__global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, float* __restrict__ out,
+                                                     int C, int H, int W, int ntr, int ntc) {
+  constexpr int P = KS / 2, IR = DW_TR + KS - 1, IC = DW_TC + KS - 1;
+  __shared__ float tile[IR][IC + 1];
+  const int plane = blockIdx.x / (ntr * ntc);
+  const int t = blockIdx.x - plane * ntr * ntc;
+  const int r0 = (t / ntc) * DW_TR, c0 = (t % ntc) * DW_TC;
+  const int c = plane % C;
+  const float* xp = x + static_cast<size_t>(plane) * H * W;
+  for (int e = threadIdx.x; e < IR * IC; e += 256) {
+    const int ir = e / IC, ic = e - ir * IC;
+    const int hh = r0 + ir - P, ww = c0 + ic - P;
+    tile[ir][ic] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xp[hh * W + ww] : 0.f;
+  }
+  float wk[KS * KS];
+#pragma unroll
+  for (int k = 0; k < KS * KS; ++k) wk[k] = w[c * KS * KS + k];   // block-uniform: scalar loads
+  __syncthreads();
+  const int col = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
+  const float b0 = bias ? bias[c] : 0.f;
+  float acc[4] = {b0, b0, b0, b0};
+#pragma unroll
+  for (int ir = 0; ir < 4 + KS - 1; ++ir) {
+    float v[KS];
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw) v[kw] = tile[rb + ir][col + kw];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int kh = ir - o;
+      if (kh >= 0 && kh < KS) {
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) acc[o] = fmaf(wk[kh * KS + kw], v[kw], acc[o]);
+      }
+    }
+  }
+  float* op = out + static_cast<size_t>(plane) * H * W;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int hh = r0 + rb + o, ww = c0 + col;
+    if (hh < H && ww < W) op[hh * W + ww] = acc[o];
+  }
+}
+
+// F.interpolate(mode="bilinear", align_corners=True): src = dst * (in-1)/(out-1)
+__global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                     long long planes, int Hi, int Wi, int Ho, int Wo, float sh,
+                                                     float sw) {
+#pragma clang fp contract(off)
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long n = planes * Ho * Wo;
+  if (i >= n) return;
+  const int ox = static_cast<int>(i % Wo);
+  const int oy = static_cast<int>((i / Wo) % Ho);
+  const long long p = i / (static_cast<long long>(Ho) * Wo);
+  const float fy = sh * oy, fx = sw * ox;
+  const int y0 = static_cast<int>(fy), x0 = static_cast<int>(fx);
+  const int y1 = y0 + (y0 < Hi - 1 ? 1 : 0), x1 = x0 + (x0 < Wi - 1 ? 1 : 0);
+  const float ly = fy - y0, lx = fx - x0;
+  const float hy = 1.f - ly, hx = 1.f - lx;
+  const float* xp = x + p * Hi * Wi;
+  const float top = hx * xp[y0 * Wi + x0] + lx * xp[y0 * Wi + x1];
+  const float bot = hx * xp[y1 * Wi + x0] + lx * xp[y1 * Wi + x1];
+  out[i] = hy * top + ly * bot;
+}
+
+}  // namespace
+}  // namespace fsmi
+
+using namespace fsmi;
+
+extern "C" int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
+                             int H, int W, void* stream) {
+  FSMI_CHECK_ARG(x && w && out, "fsmi_dwconv2d: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0, "fsmi_dwconv2d: bad shape");
+  FSMI_CHECK_ARG(KS == 3 || KS == 5 || KS == 7, "fsmi_dwconv2d: kernel %d unsupported (3, 5, 7)", KS);
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_DWCONV, s);
+  const int ntr = (H + DW_TR - 1) / DW_TR, ntc = (W + DW_TC - 1) / DW_TC;
+  const dim3 grid(static_cast<unsigned>(B) * C * ntr * ntc);
+  if (KS == 7) hipLaunchKernelGGL(dwconv_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
+  else if (KS == 5) hipLaunchKernelGGL(dwconv_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
+  else hipLaunchKernelGGL(dwconv_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
+  return finish_launch("fsmi_dwconv2d");
+}
+
+extern "C" int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo,
+                                    void* stream) {
+  FSMI_CHECK_ARG(x && out, "fsmi_resize_bilinear: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "fsmi_resize_bilinear: bad shape");
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_RESIZE, s);
+  const float sh = Ho > 1 ? static_cast<float>(Hi - 1) / static_cast<float>(Ho - 1) : 0.f;
+  const float sw = Wo > 1 ? static_cast<float>(Wi - 1) / static_cast<float>(Wo - 1) : 0.f;
+  const long long planes = static_cast<long long>(B) * C;
+  const long long n = planes * Ho * Wo;
+  hipLaunchKernelGGL(resize_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, x, out, planes,
+                     Hi, Wi, Ho, Wo, sh, sw);
+  return finish_launch("fsmi_resize_bilinear");
+}

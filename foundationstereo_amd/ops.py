@@ -384,6 +384,31 @@ def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=N
     return out
 
 
+def dwconv2d(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
+    """Depthwise conv, ``nn.Conv2d(C, C, KS, padding=KS//2, groups=C)`` (KS in 3/5/7)."""
+    _check("dwconv2d", x, w, *([bias] if bias is not None else []))
+    B, C, H, W = x.shape
+    KS = w.shape[-1]
+    assert w.shape == (C, 1, KS, KS), f"dwconv2d: weight {tuple(w.shape)} for {C} channels"
+    x, w = _c(x), _c(w)
+    out = torch.empty_like(x)
+    _lib.check(_lib.load().fsmi_dwconv2d(_p(x), _p(w), _p(_c(bias)) if bias is not None else None, _p(out), B, C,
+                                         KS, H, W, _stream(x)), "dwconv2d")
+    return out
+
+
+def resize_bilinear(x: Tensor, size) -> Tensor:
+    """``F.interpolate(x, size, mode="bilinear", align_corners=True)``."""
+    _check("resize_bilinear", x)
+    B, C, Hi, Wi = x.shape
+    Ho, Wo = size
+    x = _c(x)
+    out = torch.empty((B, C, Ho, Wo), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_resize_bilinear(_p(x), _p(out), B, C, Hi, Wi, Ho, Wo, _stream(x)),
+               "resize_bilinear")
+    return out
+
+
 # ---------------------------------------------------------------- timing
 
 def timer_enable(on: bool = True):

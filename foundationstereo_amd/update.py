@@ -9,9 +9,11 @@ packed once per (module, weight version).  The gates between the convs --
 sigmoid of z/r, ``r*h``, ``cat([r*h, x])``, ``tanh``, ``(1-z)h + zq`` and the
 ``small*att + large*(1-att)`` selection -- are two fused kernels per
 SelectiveConvGRU (``ops.gru_reset``, ``ops.gru_blend``); ``convz`` and
-``convr`` run as ONE conv with stacked weights.  Only the two 7x7 convs
-(``convd1``, the depthwise ``dwconv``) stay on MIOpen, as does everything
-under autocast (``CONV_ENGINE = "miopen"`` forces the MIOpen path for A/B).
+``convr`` run as ONE conv with stacked weights.  The two 7x7 convs run
+elsewhere: ``convd1`` (1 -> 64) on MIOpen, the depthwise ``dwconv`` on
+``ops.dwconv2d``; ``interp`` is ``ops.resize_bilinear``.  Under autocast or
+with grad enabled the module runs the plain torch path (``CONV_ENGINE =
+"miopen"`` forces it, for A/B).
 """
 from __future__ import annotations
 
@@ -72,7 +74,7 @@ class DispHead(nn.Module):
             return self.conv(x)
         y = _conv(self.conv[0], [x], "relu")
         for enc in (self.conv[2], self.conv[3]):
-            d = enc.dwconv(y)                                   # depthwise 7x7 (MIOpen); norm=None
+            d = ops.dwconv2d(y, enc.dwconv.weight, enc.dwconv.bias)   # depthwise 7x7; norm=None
             e = _conv(enc.pwconv1, [d], "gelu")
             y = _conv(enc.pwconv2, [e], gamma=enc.gamma, res=y)  # x + gamma * pw2(gelu(pw1(.)))
         return _conv(self.conv[4], [y])
@@ -138,6 +140,8 @@ def pool4x(x):
 
 
 def interp(x, dest):
+    if _fast(x):
+        return ops.resize_bilinear(x, dest.shape[2:])
     return F.interpolate(x, dest.shape[2:], mode="bilinear", align_corners=True)
 
 

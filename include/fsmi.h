@@ -171,12 +171,24 @@ int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* se
  * nsplit: split-K over 32-channel chunks (<0: auto, sized to fill the chip);
  * partial sums go to ws (nsplit*B*Cout*H*W floats, ws_floats available) and
  * a second kernel sums them in split order (deterministic) and applies the
- * epilogue.  ws may be NULL when nsplit is 0/1 (or auto: then no split). */
+ * epilogue.  ws may be NULL when nsplit is 0/1 (or auto: then no split).
+ * (A last-arriving-block fixup inside the conv kernel was measured 4x slower:
+ * the agent-scope fences it needs flush and invalidate the per-XCD L2.) */
 int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
                         const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
                         const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
                         int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
                         long long ws_floats, void* stream);
+
+/* ---- refinement-loop auxiliaries ---------------------------------------
+ * fsmi_dwconv2d: depthwise KSxKS conv (KS in {3,5,7}, stride 1, zero pad KS/2)
+ *   x, out (B,C,H,W); w (C,1,KS,KS); bias (C) or NULL.  Replaces the EdgeNeXt
+ *   dwconv of DispHead (core/submodule.py:565-591 via core/update.py:24-31).
+ * fsmi_resize_bilinear: F.interpolate(x, (Ho,Wo), mode="bilinear",
+ *   align_corners=True) on (B,C,Hi,Wi) -> (B,C,Ho,Wo) (interp, core/update.py:80). */
+int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
+                  int H, int W, void* stream);
+int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 
 /* ---- live kernel timing (bench.py roofline) -----------------------------
  * When enabled, every launch of the kernels below is bracketed by a pair of
@@ -186,7 +198,7 @@ int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const in
 enum {
   FSMI_K_GWC = 0, FSMI_K_CONCAT, FSMI_K_COMB, FSMI_K_PROJ, FSMI_K_CORR, FSMI_K_VOLPYR,
   FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
-  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_COUNT
+  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_DWCONV, FSMI_K_RESIZE, FSMI_K_COUNT
 };
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);

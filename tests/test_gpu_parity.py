@@ -163,6 +163,27 @@ def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit):
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
 
 
+@pytest.mark.parametrize("KS,shape", [(7, (2, 5, 19, 70)), (7, (1, 3, 120, 160)), (3, (1, 4, 17, 9)),
+                                      (5, (1, 2, 33, 65))])
+def test_dwconv2d_vs_torch(ops_mod, KS, shape):
+    """Depthwise conv (EdgeNeXt dwconv) vs the fp64 torch conv; ragged tiles, 1e-5 abs (49-term fp32 sums)."""
+    C = shape[1]
+    x = synth.normal(201, shape)
+    w = synth.normal(202, (C, 1, KS, KS), 0.2)
+    b = synth.normal(203, (C,), 0.1)
+    ref = torch.nn.functional.conv2d(t(x).double(), t(w).double(), t(b).double(), padding=KS // 2, groups=C)
+    close(ops_mod.dwconv2d(g(x), g(w), g(b)), ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("src,dst", [((30, 40), (60, 80)), ((60, 80), (120, 160)), ((7, 5), (13, 11)),
+                                     ((1, 6), (3, 6))])
+def test_resize_bilinear_vs_torch(ops_mod, src, dst):
+    """interp() (align_corners=True bilinear) vs the torch CPU fp32 op."""
+    x = synth.normal(211, (2, 3) + src)
+    ref = torch.nn.functional.interpolate(t(x), dst, mode="bilinear", align_corners=True)
+    close(ops_mod.resize_bilinear(g(x), dst), ref, atol=2e-6)
+
+
 # ------------------------------------------------------------------ a4 / a9
 
 def test_regression_golden(ops_mod, gold):

@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--all-cfg", action="store_true")
 ap.add_argument("--mode", default="x3", choices=["x3", "f32", "halo"])
+ap.add_argument("--nsplit", type=int, nargs="*", default=[], help="halo: also time these split-K factors")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 torch.backends.cudnn.benchmark = False
@@ -67,6 +68,8 @@ for name, cin, cout, k, H, W in SHAPES:
     t_f = timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu"))
     row = {"layer": name, "miopen_us": round(t_m, 1), "fsmi_us": round(t_f, 1),
            "fsmi_TF": round(fl / t_f / 1e6, 1), "speedup": round(t_m / t_f, 2)}
+    for ns in a.nsplit:
+        row[f"split{ns}_us"] = round(timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", nsplit=ns)), 1)
     if a.all_cfg:
         for c in range(2 if a.mode == "halo" else 4):
             row[f"cfg{c}_us"] = round(timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=c)), 1)
