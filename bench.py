@@ -104,6 +104,8 @@ def main():
                     help="MIOpen Find (exhaustive, slow first call) instead of immediate-mode heuristics")
     ap.add_argument("--mixed-precision", action="store_true",
                     help="fp16 autocast for the dense convs (the reference GPU default); volumes/lookup stay fp32")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="replay each rank's forward as one captured hipGraph (after eager warmup)")
     ap.add_argument("--conv-engine", default="fsmi", choices=["fsmi", "miopen"],
                     help="refinement-loop convs: halo-tiled split-precision MFMA kernels or MIOpen (A/B)")
     a = ap.parse_args()
@@ -153,8 +155,14 @@ def main():
     torch.cuda.synchronize()
     if rank == 0:
         print(f"[bench] setup {t_warm - t_setup:.1f}s warmup {time.perf_counter() - t_warm:.1f}s", file=sys.stderr)
-    ops.timer_enable(True)
-    ops.timer_reset()
+    if a.graph:
+        with torch.no_grad():
+            runner.capture(batch)
+        step()
+        torch.cuda.synchronize()
+    else:
+        ops.timer_enable(True)
+        ops.timer_reset()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -169,6 +177,14 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+    if a.graph:
+        # graph replays carry no per-kernel events (HIP rejects external event nodes during
+        # capture): time the kernels over one eager pass of the identical step instead
+        ops.timer_enable(True)
+        ops.timer_reset()
+        runner._graph, saved = None, runner._graph
+        step()
+        runner._graph = saved
     lk_ms, lk_n = ops.timer_query("lookup")
     cb_ms, cb_n = ops.timer_query("comb")
     ops.timer_enable(False)
@@ -206,8 +222,10 @@ def main():
         "config": {"workload": f"{a.config}: {W}x{H}, max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",
                    "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,
-                   "corr_levels": L, "conv_engine": a.conv_engine, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "geo_lookup", "bound": "hbm", "achieved": lk_bytes / lk_avg / 1e9,
+                   "corr_levels": L, "conv_engine": a.conv_engine, "hip_graph": bool(a.graph),
+                   "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "geo_lookup", "bound": "hbm",
+                     "timed_over": "eager step after the timed region" if a.graph else "timed region", "achieved": lk_bytes / lk_avg / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
                      "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,
                      "launches": lk_n},

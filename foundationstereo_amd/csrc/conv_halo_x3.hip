@@ -266,6 +266,40 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
   a.out[b * a.out_bstride + (a.co0 + co) * HW + hw] = v;
 }
 
+// Vector form (H*W % 4 == 0): one (b, co) plane per blockIdx.y, float4 per thread,
+// all nsplit partial loads in flight before the ordered sum.
+__global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
+  const int HW = a.H * a.W;
+  const int hw = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (hw >= HW) return;
+  const int plane = blockIdx.y, co = plane % a.Cout, b = plane / a.Cout;
+  const size_t n = static_cast<size_t>(a.B) * a.Cout * HW;
+  const float* src = a.ws + static_cast<size_t>(plane) * HW + hw;
+  float4 p[8];
+#pragma unroll
+  for (int sp = 0; sp < 8; ++sp)
+    if (sp < a.nsplit) p[sp] = *reinterpret_cast<const float4*>(src + sp * n);
+  float4 v = p[0];
+#pragma unroll
+  for (int sp = 1; sp < 8; ++sp)
+    if (sp < a.nsplit) { v.x += p[sp].x; v.y += p[sp].y; v.z += p[sp].z; v.w += p[sp].w; }
+  const float bb = a.bias ? a.bias[co] : 0.f;
+  float r[4] = {v.x + bb, v.y + bb, v.z + bb, v.w + bb};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (a.act == 1) r[k] = fmaxf(r[k], 0.f);
+    else if (a.act == 2) r[k] = gelu_erf_h(r[k]);
+    r[k] *= a.alpha;
+    if (a.gamma) r[k] *= a.gamma[co];
+  }
+  if (a.res) {
+    const float4 q = *reinterpret_cast<const float4*>(a.res + b * a.res_bstride + static_cast<size_t>(co) * HW + hw);
+    r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
+  }
+  *reinterpret_cast<float4*>(a.out + b * a.out_bstride + static_cast<size_t>(a.co0 + co) * HW + hw) =
+      make_float4(r[0], r[1], r[2], r[3]);
+}
+
 template <int KS, int BM, int TR, int WM>
 void tile_counts(HaloArgs& a) {
   a.nrt = (a.H + TR - 1) / TR;
@@ -279,8 +313,17 @@ int launch_halo(HaloArgs a, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
   hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
   if (a.nsplit > 1) {
-    const long long n = static_cast<long long>(a.B) * a.Cout * a.H * a.W;
-    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, a);
+    const int HW = a.H * a.W;
+    const bool vec = HW % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(a.ws) % 16 == 0 &&
+                     (!a.res || reinterpret_cast<uintptr_t>(a.res) % 16 == 0);
+    if (vec) {
+      hipLaunchKernelGGL(conv_split_reduce4_kernel, dim3((HW / 4 + 255) / 256, a.B * a.Cout), dim3(256), 0, s, a);
+    } else {
+      const long long n = static_cast<long long>(a.B) * a.Cout * HW;
+      hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
+                         a);
+    }
   }
   return finish_launch("fsmi_conv2d_halo_x3");
 }

@@ -40,9 +40,15 @@ def autocast(enabled, dtype="float16"):
 
 def normalize_image(img):
     """(x/255 - mean)/std per RGB channel (core/foundation_stereo.py:37-42)."""
-    mean = torch.tensor(_MEAN, device=img.device, dtype=img.dtype).view(1, 3, 1, 1)
-    std = torch.tensor(_STD, device=img.device, dtype=img.dtype).view(1, 3, 1, 1)
+    key = (img.device, img.dtype)
+    if key not in _NORM_CACHE:     # device constants made once (an H2D copy cannot be graph-captured)
+        _NORM_CACHE[key] = (torch.tensor(_MEAN, device=img.device, dtype=img.dtype).view(1, 3, 1, 1),
+                            torch.tensor(_STD, device=img.device, dtype=img.dtype).view(1, 3, 1, 1))
+    mean, std = _NORM_CACHE[key]
     return ((img / 255.0 - mean) / std).contiguous()
+
+
+_NORM_CACHE = {}
 
 
 class hourglass(nn.Module):
