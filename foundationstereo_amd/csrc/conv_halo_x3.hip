@@ -7,13 +7,19 @@
 //   * per 32-channel chunk the (TR+2) x 34 input halo is loaded ONCE, split
 //     into fp16 hi/lo and kept in LDS for all 9 taps (fragments for tap
 //     (dh,dw) are the halo rows/cols shifted by (dh,dw));
-//   * per tap the BM x 32 weight slice (pre-split, pre-packed) goes through a
-//     double-buffered LDS slot whose next fill is in flight during the MFMAs;
+//   * weights (pre-split, pre-packed) either go per tap through a double-
+//     buffered LDS slot whose next fill is in flight during the MFMAs
+//     (conv_halo_x3_kernel, cfg 0/1: one barrier per tap), or each wave loads
+//     its own A fragments from L2 into a double-buffered register set one tap
+//     ahead (conv_halo_wreg_kernel, cfg 2/3: LDS holds only the halo, two
+//     barriers per 32-channel chunk);
 //   * blocks are ordered cout-tile-major over an XCD-aware remap, so each XCD
 //     works on one cout slice and keeps its weights in its 4 MB L2.
 // MFMA v_mfma_f32_32x32x16_f16, three per product (lo*hi, hi*lo, hi*hi), fp32
 // accumulation; fragment maps as in conv2d_x3.hip.  Epilogue identical to
 // fsmi_conv2d (bias, ReLU/GELU, alpha, gamma, residual, channel-offset store).
+#include <type_traits>
+
 #include "fsmi_common.h"
 
 namespace fsmi {
@@ -21,6 +27,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 
 constexpr int HKC = 32;            // channels per chunk
 constexpr int HROW = HKC + 8;      // padded LDS row (halves): conflict-free ds_read_b128 at 80-B stride
@@ -49,189 +56,149 @@ struct HaloArgs {
 
 __device__ __forceinline__ float gelu_erf_h(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
-template <int KS, int BM, int TR, int WM>
-__global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
-  constexpr int WN = 4 / WM;
-  constexpr int TM = BM / WM / 32, TN = TR / WN;
-  constexpr int PD = KS / 2;
-  constexpr int HR = TR + KS - 1, HC = 32 + KS - 1, NHP = HR * HC;
-  constexpr int NTAP = KS * KS;
-  constexpr int W_PIECES = BM * HKC / 8;           // 16-B pieces per hi (or lo) weight slice
-  constexpr int W_PER_T = (W_PIECES + 255) / 256;
-  constexpr int X_TASKS = NHP * (HKC / 8);
-  constexpr int X_PER_T = (X_TASKS + 255) / 256;
-  __shared__ __attribute__((aligned(16))) _Float16 Xh[NHP][HROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Xl[NHP][HROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Wh[2][BM][HROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Wl[2][BM][HROW];
+// ---------------------------------------------------------------- shared pieces
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave % WM, wn = wave / WM;
-  const int hsel = lane >> 5, rl = lane & 31;
-  // cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
-  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
-  const int cs = item / a.npix;             // (cout tile, split) pair
-  const int ptile = item - cs * a.npix;
-  const int ctile = cs / a.nsplit, split = cs - ctile * a.nsplit;
-  const int m0 = ctile * BM;
-  const int b = ptile / (a.nrt * a.nct);
-  const int prem = ptile - b * a.nrt * a.nct;
-  const int r0 = (prem / a.nct) * TR, c0 = (prem % a.nct) * 32;
-  const int HW = a.H * a.W;
-  const int nck = a.CinP / HKC;
+// Input-halo staging for a TR x 32 pixel tile: task = (halo pixel, 8-channel
+// group); per task a packed descriptor (clamped pixel offset << 3 | in-image << 2
+// | group) computed once per block; a chunk is loaded into registers one chunk
+// ahead and split into fp16 hi/lo when stored to LDS.
+template <int KS, int TR>
+struct HaloStage {
+  static constexpr int PD = KS / 2, HR = TR + KS - 1, HC = 32 + KS - 1, NHP = HR * HC;
+  static constexpr int X_TASKS = NHP * (HKC / 8), X_PER_T = (X_TASKS + 255) / 256;
+  int desc[X_PER_T];
+  f32x8 xv[X_PER_T];
 
-  uint4 rwh[W_PER_T], rwl[W_PER_T];
-  auto load_w = [&](int cc, int tap) {
-    const size_t base = (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
-#pragma unroll
-    for (int u = 0; u < W_PER_T; ++u) {
-      const int e = tid + 256 * u;
-      rwh[u] = rwl[u] = make_uint4(0, 0, 0, 0);
-      if (e < W_PIECES) {
-        const int m = e / (HKC / 8), q = e - m * (HKC / 8);
-        if (m0 + m < a.CoutP) {
-          const size_t off = base + static_cast<size_t>(m0 + m) * HKC + q * 8;
-          rwh[u] = *reinterpret_cast<const uint4*>(a.whi + off);
-          rwl[u] = *reinterpret_cast<const uint4*>(a.wlo + off);
-        }
-      }
-    }
-  };
-  auto store_w = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < W_PER_T; ++u) {
-      const int e = tid + 256 * u;
-      if (e < W_PIECES) {
-        const int m = e / (HKC / 8), q = e - m * (HKC / 8);
-        *reinterpret_cast<uint4*>(&Wh[buf][m][q * 8]) = rwh[u];
-        *reinterpret_cast<uint4*>(&Wl[buf][m][q * 8]) = rwl[u];
-      }
-    }
-  };
-  // halo chunk -> registers (issued a whole chunk ahead), then split into LDS
-  float xv[X_PER_T][8];
-  auto load_halo = [&](int cc) {
+  __device__ __forceinline__ void init(const HaloArgs& a, int tid, int r0, int c0) {
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u) {
-      const int task = tid + 256 * u;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xv[u][j] = 0.f;
-      if (task < X_TASKS) {
-        const int hp = task % NHP, g = task / NHP;
-        const int hr = hp / HC, hc = hp - hr * HC;
-        const int hh = r0 + hr - PD, ww = c0 + hc - PD;
-        const int ci0 = cc * HKC + g * 8;
-        if (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W && ci0 < a.Cin) {
-          int s = 0, base = 0;   // segments are multiples of 8 channels: one lookup per group
-#pragma unroll
-          for (int q = 0; q < kHMaxSeg - 1; ++q)
-            if (q < a.nseg - 1 && ci0 >= a.seg_end[q]) { s = q + 1; base = a.seg_end[q]; }
-          const float* src = a.seg_ptr[s] + b * a.seg_bstride[s] + static_cast<long long>(ci0 - base) * HW +
-                             hh * a.W + ww;
-          const int nv = min(8, a.Cin - ci0);
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (j < nv) xv[u][j] = src[static_cast<size_t>(j) * HW];
-        }
-      }
+      const int task = min(tid + 256 * u, X_TASKS - 1);
+      const int hp = task % NHP, g = task / NHP;
+      const int hr = hp / HC, hc = hp - hr * HC;
+      const int hh = r0 + hr - PD, ww = c0 + hc - PD;
+      const bool in = hh >= 0 && hh < a.H && ww >= 0 && ww < a.W && tid + 256 * u < X_TASKS;
+      const int pix = min(max(hh, 0), a.H - 1) * a.W + min(max(ww, 0), a.W - 1);
+      desc[u] = (pix << 3) | (in ? 4 : 0) | g;
     }
-  };
-  auto store_halo = [&]() {
+  }
+
+  __device__ __forceinline__ void load(const HaloArgs& a, int b, int cc) {
+    const int HW = a.H * a.W;
+    const bool full = (cc + 1) * HKC <= a.Cin;     // block-uniform: only the last chunk is ragged
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u) {
-      const int task = tid + 256 * u;
-      if (task < X_TASKS) {
-        const int hp = task % NHP, g = task / NHP;
-        half8 hi, lo;
+      const int g = desc[u] & 3, pix = desc[u] >> 3;
+      const int ci0 = cc * HKC + g * 8;
+      const int cic = min(ci0, a.Cin - 1);
+      // segment of this 8-channel group (segments hold multiples of 8 channels): a select
+      // chain over constant indices, so the kernarg arrays are never indexed per lane
+      const float* sp = a.seg_ptr[0];
+      long long sb = a.seg_bstride[0];
+      int base = 0;
+#pragma unroll
+      for (int q = 1; q < kHMaxSeg; ++q) {
+        const bool in_q = q < a.nseg && cic >= a.seg_end[q - 1];
+        sp = in_q ? a.seg_ptr[q] : sp;
+        sb = in_q ? a.seg_bstride[q] : sb;
+        base = in_q ? a.seg_end[q - 1] : base;
+      }
+      const float* src = sp + b * sb + static_cast<long long>(cic - base) * HW + pix;
+      const bool ok = desc[u] & 4;
+      f32x8 v;
+      if (full) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = src[static_cast<size_t>(j) * HW];
+      } else {
+        const int nv = a.Cin - ci0;                // may be <= 0 in the padded tail
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const _Float16 x16 = static_cast<_Float16>(xv[u][j]);
-          hi[j] = x16;
-          lo[j] = static_cast<_Float16>(xv[u][j] - static_cast<float>(x16));
+          const float t = src[static_cast<size_t>(max(0, min(j, nv - 1))) * HW];
+          v[j] = j < nv ? t : 0.f;
         }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[u][j] = ok ? v[j] : 0.f;
+    }
+  }
+
+  __device__ __forceinline__ void store(_Float16 (*Xh)[HROW], _Float16 (*Xl)[HROW], int tid) const {
+#pragma unroll
+    for (int u = 0; u < X_PER_T; ++u) {
+      const int task = tid + 256 * u;
+      if (X_TASKS % 256 == 0 || task < X_TASKS) {
+        const int hp = task % NHP, g = task / NHP;
+        const half8 hi = __builtin_convertvector(xv[u], half8);
+        const half8 lo = __builtin_convertvector(xv[u] - __builtin_convertvector(hi, f32x8), half8);
         *reinterpret_cast<half8*>(&Xh[hp][g * 8]) = hi;
         *reinterpret_cast<half8*>(&Xl[hp][g * 8]) = lo;
       }
     }
-  };
+  }
+};
 
-  f32x16 acc[TM][TN];
+struct TileCoord {
+  int m0, b, r0, c0, split;
+};
+
+// cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
+template <int BM, int TR>
+__device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int cs = item / a.npix;                    // (cout tile, split) pair
+  const int ptile = item - cs * a.npix;
+  const int ctile = cs / a.nsplit;
+  TileCoord t;
+  t.split = cs - ctile * a.nsplit;
+  t.m0 = ctile * BM;
+  t.b = ptile / (a.nrt * a.nct);
+  const int prem = ptile - t.b * a.nrt * a.nct;
+  t.r0 = (prem / a.nct) * TR;
+  t.c0 = (prem % a.nct) * 32;
+  return t;
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM], const half8 (&al)[TM],
+                                     const half8 (&bh)[TN], const half8 (&bl)[TN]) {
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // split-K: this block reduces channel chunks [cc_begin, cc_end)
-  const int cc_begin = split * a.kpc;
-  const int cc_end = min(nck, cc_begin + a.kpc);
-  int step = 0;
-  load_w(cc_begin, 0);
-  load_halo(cc_begin);
-  for (int cc = cc_begin; cc < cc_end; ++cc) {
-    __syncthreads();               // every wave is done with the previous chunk's halo
-    store_halo();
-    if (cc + 1 < cc_end) load_halo(cc + 1);   // in flight during this chunk's taps
-#pragma unroll 1
-    for (int tap = 0; tap < NTAP; ++tap, ++step) {
-      const int buf = step & 1;
-      store_w(buf);
-      __syncthreads();             // halo (first tap) and this tap's weights visible
-      if (tap + 1 < NTAP) load_w(cc, tap + 1);
-      else if (cc + 1 < cc_end) load_w(cc + 1, 0);
-      const int dh = tap / KS, dw = tap % KS;
-#pragma unroll
-      for (int ks = 0; ks < HKC; ks += 16) {
-        half8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int m = (wm * TM + i) * 32 + rl;
-          ah[i] = *reinterpret_cast<const half8*>(&Wh[buf][m][ks + 8 * hsel]);
-          al[i] = *reinterpret_cast<const half8*>(&Wl[buf][m][ks + 8 * hsel]);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int hp = ((wn * TN + j) + dh) * HC + rl + dw;
-          bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][ks + 8 * hsel]);
-          bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][ks + 8 * hsel]);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-          }
-      }
+    for (int j = 0; j < TN; ++j) {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
     }
-  }
+}
 
-  // epilogue: n = lane&31 is the pixel column, rows of the tile on j
+// n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
+template <int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], const TileCoord& t,
+                                              int wm, int wn, int lane) {
+  const int hsel = lane >> 5, rl = lane & 31;
+  const int HW = a.H * a.W;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int hh = r0 + wn * TN + j, ww = c0 + rl;
+    const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
     if (hh >= a.H || ww >= a.W) continue;
     const int hw = hh * a.W + ww;
-    if (a.nsplit > 1) {            // raw partial sums; conv_split_reduce_kernel applies the epilogue
-      float* wp = a.ws + (static_cast<size_t>(split) * a.B + b) * a.Cout * HW + hw;
+    if (a.nsplit > 1) {            // raw partial sums; the split reduce applies the epilogue
+      float* wp = a.ws + (static_cast<size_t>(t.split) * a.B + t.b) * a.Cout * HW + hw;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int co = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+          const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
           if (co < a.Cout) wp[static_cast<size_t>(co) * HW] = acc[i][j][r] * a.wscale;
         }
       continue;
     }
-    float* ob = a.out + b * a.out_bstride + hw;
-    const float* rbp = a.res ? a.res + b * a.res_bstride + hw : nullptr;
+    float* ob = a.out + t.b * a.out_bstride + hw;
+    const float* rbp = a.res ? a.res + t.b * a.res_bstride + hw : nullptr;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+        const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
         if (co >= a.Cout) continue;
         float v = acc[i][j][r] * a.wscale;
         if (a.bias) v += a.bias[co];
@@ -244,6 +211,221 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
       }
     }
   }
+}
+
+// ---------------------------------------------------------------- cfg 0/1: weights through LDS
+
+template <int KS, int BM, int TR, int WM>
+__global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32, TN = TR / WN;
+  constexpr int NTAP = KS * KS;
+  constexpr int W_PIECES = BM * HKC / 8;           // 16-B pieces per hi (or lo) weight slice
+  constexpr int W_PER_T = W_PIECES / 256;
+  static_assert(W_PIECES % 256 == 0, "weight pieces must tile the block");
+  using HS = HaloStage<KS, TR>;
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Wh[2][BM][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Wl[2][BM][HROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int hsel = lane >> 5, rl = lane & 31;
+  const TileCoord tc = decode_tile<BM, TR>(a);
+  const int m0 = tc.m0;
+  const int nck = a.CinP / HKC;
+
+  const bool w_full = m0 + BM <= a.CoutP;          // block-uniform: only the last cout tile is ragged
+  uint4 rwh[W_PER_T], rwl[W_PER_T];
+  auto load_w = [&](int cc, int tap) {
+    const size_t base = (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+    const _Float16* ph = a.whi + base;
+    const _Float16* pl = a.wlo + base;
+    if (w_full) {
+#pragma unroll
+      for (int u = 0; u < W_PER_T; ++u) {
+        const int e = tid + 256 * u;
+        const int off = (m0 + e / (HKC / 8)) * HKC + (e % (HKC / 8)) * 8;
+        rwh[u] = *reinterpret_cast<const uint4*>(ph + off);
+        rwl[u] = *reinterpret_cast<const uint4*>(pl + off);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < W_PER_T; ++u) {
+        const int e = tid + 256 * u;
+        const int row = m0 + e / (HKC / 8);
+        const int off = min(row, a.CoutP - 1) * HKC + (e % (HKC / 8)) * 8;   // clamped, then zeroed
+        const uint4 h = *reinterpret_cast<const uint4*>(ph + off);
+        const uint4 l = *reinterpret_cast<const uint4*>(pl + off);
+        const bool ok = row < a.CoutP;             // per component: a uint4 ternary goes via scratch
+        rwh[u] = make_uint4(ok ? h.x : 0u, ok ? h.y : 0u, ok ? h.z : 0u, ok ? h.w : 0u);
+        rwl[u] = make_uint4(ok ? l.x : 0u, ok ? l.y : 0u, ok ? l.z : 0u, ok ? l.w : 0u);
+      }
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < W_PER_T; ++u) {
+      const int e = tid + 256 * u;
+      const int m = e / (HKC / 8), q = e % (HKC / 8);
+      *reinterpret_cast<uint4*>(&Wh[buf][m][q * 8]) = rwh[u];
+      *reinterpret_cast<uint4*>(&Wl[buf][m][q * 8]) = rwl[u];
+    }
+  };
+  HS hs;
+  hs.init(a, tid, tc.r0, tc.c0);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // split-K: this block reduces channel chunks [cc_begin, cc_end)
+  const int cc_begin = tc.split * a.kpc;
+  const int cc_end = min(nck, cc_begin + a.kpc);
+  int step = 0;
+  load_w(cc_begin, 0);
+  hs.load(a, tc.b, cc_begin);
+  for (int cc = cc_begin; cc < cc_end; ++cc) {
+    __syncthreads();               // every wave is done with the previous chunk's halo
+    hs.store(Xh, Xl, tid);
+    if (cc + 1 < cc_end) hs.load(a, tc.b, cc + 1);   // in flight during this chunk's taps
+#pragma unroll 1
+    for (int tap = 0; tap < NTAP; ++tap, ++step) {
+      const int buf = step & 1;
+      store_w(buf);
+      __syncthreads();             // halo (first tap) and this tap's weights visible
+      // next slice; past the end it re-loads the last one (unconditional, never used)
+      const bool wrap = tap + 1 == NTAP;
+      load_w(wrap ? min(cc + 1, cc_end - 1) : cc, wrap ? 0 : tap + 1);
+      const int dh = tap / KS, dw = tap % KS;
+#pragma unroll
+      for (int ks = 0; ks < HKC; ks += 16) {
+        half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = (wm * TM + i) * 32 + rl;
+          ah[i] = *reinterpret_cast<const half8*>(&Wh[buf][m][ks + 8 * hsel]);
+          al[i] = *reinterpret_cast<const half8*>(&Wl[buf][m][ks + 8 * hsel]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+          bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][ks + 8 * hsel]);
+          bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][ks + 8 * hsel]);
+        }
+        mma3<TM, TN>(acc, ah, al, bh, bl);
+      }
+    }
+  }
+  conv_epilogue<TM, TN>(a, acc, tc, wm, wn, lane);
+}
+
+// ---------------------------------------------------------------- cfg 2/3: weights in registers
+
+template <int KS, int BM, int TR, int WM>
+__global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32, TN = TR / WN;
+  constexpr int NTAP = KS * KS;
+  using HS = HaloStage<KS, TR>;
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int hsel = lane >> 5, rl = lane & 31;
+  const TileCoord tc = decode_tile<BM, TR>(a);
+  const int nck = a.CinP / HKC;
+
+  // this lane's A-fragment rows (rows past Cout only feed outputs the epilogue drops:
+  // clamped so every address is mapped, no zeroing needed)
+  int wrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) wrow[i] = min(tc.m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
+  half8 wf[2][TM][2][2];           // [buffer][i][k half][hi, lo]
+  auto load_wf = [&](auto buf_c, int cc, int tap) {
+    constexpr int buf = decltype(buf_c)::value;
+    const size_t base = (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
+        wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+      }
+  };
+  HS hs;
+  hs.init(a, tid, tc.r0, tc.c0);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int cc_begin = tc.split * a.kpc;
+  const int cc_end = min(nck, cc_begin + a.kpc);
+  // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
+  auto chunk = [&](auto par_c, int cc) {
+    constexpr int P = decltype(par_c)::value;
+#pragma unroll
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const bool last = tap + 1 == NTAP;
+      if (((tap + P) & 1) == 0) {
+        load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+      } else {
+        load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+      }
+      const int dh = tap / KS, dw = tap % KS;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          ah[i] = wf[(tap + P) & 1][i][k][0];
+          al[i] = wf[(tap + P) & 1][i][k][1];
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+          bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][16 * k + 8 * hsel]);
+          bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][16 * k + 8 * hsel]);
+        }
+        mma3<TM, TN>(acc, ah, al, bh, bl);
+      }
+      // keep the one-tap-ahead structure: without this fence the scheduler hoists every
+      // tap's loads of the unrolled chunk to its top (500 registers, 1 wave per SIMD)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto stage = [&](int cc) {
+    __syncthreads();               // every wave is done with the previous chunk's halo
+    hs.store(Xh, Xl, tid);
+    if (cc + 1 < cc_end) hs.load(a, tc.b, cc + 1);   // in flight during this chunk's taps
+    __syncthreads();
+  };
+  load_wf(std::integral_constant<int, 0>(), cc_begin, 0);
+  hs.load(a, tc.b, cc_begin);
+  // chunks in pairs so every register-buffer index is static (parity 0, then 1)
+  int cc = cc_begin;
+  for (; cc + 1 < cc_end; cc += 2) {
+    stage(cc);
+    chunk(std::integral_constant<int, 0>(), cc);
+    stage(cc + 1);
+    chunk(std::integral_constant<int, 1>(), cc + 1);
+  }
+  if (cc < cc_end) {
+    stage(cc);
+    chunk(std::integral_constant<int, 0>(), cc);
+  }
+  conv_epilogue<TM, TN>(a, acc, tc, wm, wn, lane);
 }
 
 // Sums the split-K partials in split order (deterministic) and applies the epilogue.
@@ -308,10 +490,11 @@ void tile_counts(HaloArgs& a) {
   a.nco = (a.Cout + BM - 1) / BM;
 }
 
-template <int KS, int BM, int TR, int WM>
+template <int KS, int BM, int TR, int WM, bool WREG>
 int launch_halo(HaloArgs a, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
-  hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
+  if (WREG) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
   if (a.nsplit > 1) {
     const int HW = a.H * a.W;
     const bool vec = HW % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
@@ -380,8 +563,12 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_CONV2D, s);
-  if (cfg < 0) cfg = (Cout > 64) ? 1 : 0;
-  if (cfg == 1) tile_counts<3, 128, 4, 2>(a);
+  // default tiles, measured per layer shape (tools/conv_bench.py --all-cfg): 3x3 layers run best
+  // with register-resident weights (128 couts, or 64 for narrow outputs), 1x1 layers -- one tap
+  // per chunk, so the per-tap LDS barrier is no cost -- with LDS weights and 128 couts
+  if (cfg < 0) cfg = KS == 3 ? (Cout > 64 ? 3 : 2) : (Cout > 64 ? 1 : 0);
+  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 3, "fsmi_conv2d_halo_x3: cfg %d (0..3)", cfg);
+  if (cfg & 1) tile_counts<3, 128, 4, 2>(a);      // odd cfgs: 128 couts x 4x32 px; even: 64 x 8x32
   else tile_counts<3, 64, 8, 1>(a);
   // split-K when the output tiles alone cannot fill 256 CUs x 2 resident blocks
   const int nck = a.CinP / HKC;
@@ -402,6 +589,18 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
   FSMI_CHECK_ARG(a.nsplit == 1 || (ws && per_split * a.nsplit <= ws_floats),
                  "fsmi_conv2d_halo_x3: split-K %d needs %lld workspace floats", a.nsplit, per_split * a.nsplit);
   a.ws = ws;
-  if (KS == 3) return cfg == 1 ? launch_halo<3, 128, 4, 2>(a, s) : launch_halo<3, 64, 8, 1>(a, s);
-  return cfg == 1 ? launch_halo<1, 128, 4, 2>(a, s) : launch_halo<1, 64, 8, 1>(a, s);
+  if (KS == 3) {
+    switch (cfg) {
+      case 0: return launch_halo<3, 64, 8, 1, false>(a, s);
+      case 1: return launch_halo<3, 128, 4, 2, false>(a, s);
+      case 2: return launch_halo<3, 64, 8, 1, true>(a, s);
+      default: return launch_halo<3, 128, 4, 2, true>(a, s);
+    }
+  }
+  switch (cfg) {
+    case 0: return launch_halo<1, 64, 8, 1, false>(a, s);
+    case 1: return launch_halo<1, 128, 4, 2, false>(a, s);
+    case 2: return launch_halo<1, 64, 8, 1, true>(a, s);
+    default: return launch_halo<1, 128, 4, 2, true>(a, s);
+  }
 }

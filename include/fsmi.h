@@ -167,7 +167,9 @@ int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* se
 /* Halo-tiled variant of fsmi_conv2d_x3 (same weights, same epilogue) for
  * square KS in {1, 3}: a block stages a (rows+2)x34 input halo once per
  * 32-channel chunk and runs all taps from LDS.  Inner segments must hold a
- * multiple of 8 channels.  cfg 0: 64 couts x 8x32 px; 1: 128 couts x 4x32 px.
+ * multiple of 8 channels.  cfg 0: 64 couts x 8x32 px, 1: 128 couts x 4x32 px
+ * (weights staged per tap through LDS); 2 / 3: the same tiles with each wave's
+ * weight fragments loaded into registers one tap ahead; -1: measured default.
  * nsplit: split-K over 32-channel chunks (<0: auto, sized to fill the chip);
  * partial sums go to ws (nsplit*B*Cout*H*W floats, ws_floats available) and
  * a second kernel sums them in split order (deterministic) and applies the

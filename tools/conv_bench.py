@@ -20,6 +20,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--all-cfg", action="store_true")
 ap.add_argument("--mode", default="x3", choices=["x3", "f32", "halo"])
+ap.add_argument("--cfg", type=int, default=-1, help="tile config for the main timing (-1 auto)")
+ap.add_argument("--only", default="", help="comma-separated layer names")
+ap.add_argument("--no-miopen", action="store_true")
 ap.add_argument("--nsplit", type=int, nargs="*", default=[], help="halo: also time these split-K factors")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
@@ -59,19 +62,21 @@ tot_m = tot_f = 0.0
 for name, cin, cout, k, H, W in SHAPES:
     if a.mode == "halo" and k not in (1, 3):
         continue
+    if a.only and name not in a.only.split(","):
+        continue
     x = torch.randn(1, cin, H, W, device=dev)
     w = torch.randn(cout, cin, k, k, device=dev) * 0.05
     b = torch.randn(cout, device=dev)
     pk = ops.PackedConv(w, mode=a.mode)
     fl = 2.0 * cin * cout * k * k * H * W
-    t_m = timeit(lambda: F.relu(F.conv2d(x, w, b, padding=k // 2)))
-    t_f = timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu"))
+    t_m = 1.0 if a.no_miopen else timeit(lambda: F.relu(F.conv2d(x, w, b, padding=k // 2)))
+    t_f = timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=a.cfg))
     row = {"layer": name, "miopen_us": round(t_m, 1), "fsmi_us": round(t_f, 1),
            "fsmi_TF": round(fl / t_f / 1e6, 1), "speedup": round(t_m / t_f, 2)}
     for ns in a.nsplit:
         row[f"split{ns}_us"] = round(timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", nsplit=ns)), 1)
     if a.all_cfg:
-        for c in range(2 if a.mode == "halo" else 4):
+        for c in range(4):
             row[f"cfg{c}_us"] = round(timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=c)), 1)
     rows.append(row)
     tot_m += t_m
