@@ -36,6 +36,7 @@ from foundationstereo_amd import dist as fdist  # noqa: E402
 from foundationstereo_amd import synth  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, B/s (MI355X_MICROARCH.md chip table)
+MFMA_F16_PEAK = 2.5e15  # dense fp16 MFMA, FLOP/s (MI355X_MICROARCH.md; no sparsity)
 
 # BASELINE.json configs (name -> H, W, max_disp, iters, vit, pairs per GPU)
 CONFIGS = {
@@ -187,6 +188,8 @@ def main():
         runner._graph = saved
     lk_ms, lk_n = ops.timer_query("lookup")
     cb_ms, cb_n = ops.timer_query("comb")
+    cv_ms, cv_n = ops.timer_query("conv2d")
+    cv_flops = ops.conv_flops()
     ops.timer_enable(False)
     assert torch.isfinite(out).all()
 
@@ -229,6 +232,13 @@ def main():
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
                      "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,
                      "launches": lk_n},
+        # the refinement-loop convs (halo-tiled 3 x fp16 MFMA, split-K reduce included) hold most of
+        # the step time; algorithmic = fp32 conv FLOPs, peak = dense fp16 MFMA / 3 products per MAC
+        "roofline_conv": {"kernel": "conv2d_halo_x3 (all loop convs)", "bound": "mfma",
+                          "achieved": cv_flops / (cv_ms / 1e3) / 1e12 if cv_n else None,
+                          "peak": MFMA_F16_PEAK / 3 / 1e12, "unit": "TFLOP/s",
+                          "frac": cv_flops / (cv_ms / 1e3) / (MFMA_F16_PEAK / 3) if cv_n else None,
+                          "algorithmic_flops": cv_flops, "total_ms": cv_ms, "launches": cv_n},
         "roofline_build": {"kernel": "comb_volume_stem", "bound": "hbm",
                            "achieved": cb_bytes / cb_avg / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
                            "unit": "GB/s", "frac": cb_bytes / cb_avg / HBM_PEAK if cb_n else None,

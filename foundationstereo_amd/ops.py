@@ -369,6 +369,8 @@ def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=N
               _p(res) if res is not None else None, res.shape[1] if res is not None else 0,
               _p(out), out.shape[1], co0, B, pk.cout, pk.k, pk.k, H, W, ACT[act], float(alpha), cfg, _stream(t0))
     lib = _lib.load()
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * cin * pk.cout * pk.k * pk.k * B * H * W
     if pk.mode == "f32":
         _lib.check(lib.fsmi_conv2d(pp, chs, tots, len(norm), _p(pk.wpk), *common), "conv2d")
     elif pk.mode == "x3":
@@ -411,12 +413,23 @@ def resize_bilinear(x: Tensor, size) -> Tensor:
 
 # ---------------------------------------------------------------- timing
 
+# algorithmic fp32 conv FLOPs (2*Cin*Cout*k*k*B*H*W) of the conv2d calls made since the last
+# timer_reset() while timers are enabled -- the numerator of bench.py's conv roofline
+_CONV_FLOPS = {"on": False, "flops": 0}
+
+
 def timer_enable(on: bool = True):
     _lib.check(_lib.load().fsmi_timer_enable(1 if on else 0), "timer_enable")
+    _CONV_FLOPS["on"] = bool(on)
 
 
 def timer_reset():
     _lib.check(_lib.load().fsmi_timer_reset(), "timer_reset")
+    _CONV_FLOPS["flops"] = 0
+
+
+def conv_flops() -> int:
+    return _CONV_FLOPS["flops"]
 
 
 def timer_query(kernel: str):
