@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from . import update as _update
 from .extractor import ContextNetDino, SyntheticFeature
 from .geometry import Combined_Geo_Encoding_Volume
 from .submodule import (BasicConv, BasicConv_IN, ChannelAttentionEnhancement, Conv2x, Conv3dNormActReduced,
@@ -220,11 +221,16 @@ class FoundationStereo(nn.Module):
         disp = init_disp.float()
         disp_preds = []
         disp_up = None
+        overlap = not mp and _update._fast(disp)
         for itr in range(iters):
             disp = disp.detach()
-            geo_feat = geo_fn(disp)
-            with autocast(mp, md):
-                net_list, mask_feat_4, delta_disp = self.update_block(net_list, inp_list, geo_feat, disp, att)
+            if overlap:    # lookup + motion encoder on a side stream beside gru16/gru08 (same math)
+                net_list, mask_feat_4, delta_disp = self.update_block.forward_overlapped(
+                    net_list, inp_list, geo_fn, disp, att)
+            else:
+                geo_feat = geo_fn(disp)
+                with autocast(mp, md):
+                    net_list, mask_feat_4, delta_disp = self.update_block(net_list, inp_list, geo_feat, disp, att)
             disp = disp + delta_disp.float()
             if test_mode and itr < iters - 1:
                 continue

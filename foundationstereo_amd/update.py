@@ -48,6 +48,16 @@ def _packed(*mods):
     return hit[1], hit[2]
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
 def _conv(mods, segs, act=None, **kw):
     mods = mods if isinstance(mods, tuple) else (mods,)
     pk, bias = _packed(*mods)
@@ -250,6 +260,36 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             net[0] = self.gru04(att[0], net[0], motion, interp(net[1], net[0]))
         delta_disp = self.disp_head(net[0])
         mask = .25 * self.mask(net[0])
+        return net, mask, delta_disp
+
+    def forward_overlapped(self, net, inp, geo_fn, disp, att):
+        """``forward(net, inp, geo_fn(disp), disp, att)`` with the motion path -- the lookup and
+        the motion encoder, which depend only on ``disp`` -- on a side stream, concurrently with
+        gru16 / gru08 (small 1/16 and 1/8 maps that leave most CUs idle).  Joined before gru04.
+        Cross-stream buffers (``enc``) are allocated on the calling stream and ``disp`` is only
+        released by the caller after the join, so the caching allocator never recycles memory a
+        pending side-stream kernel still reads.  Captures into a hipGraph as a fork/join."""
+        main = torch.cuda.current_stream(disp.device)
+        side = _side_stream(disp.device)
+        B, _, H, W = disp.shape
+        enc = disp.new_empty(B, self.encoder.conv.out_channels + 1, H, W)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            corr = geo_fn(disp)
+            self.encoder.encode_into(disp, corr, enc)
+        n = self.args.n_gru_layers
+        if n == 3:
+            net[2] = self.gru16(att[2], net[2], inp[2], pool2x(net[1]))
+        if n >= 2:
+            if n > 2:
+                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]), interp(net[2], net[1]))
+            else:
+                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]))
+        main.wait_stream(side)
+        if n > 1:
+            net[0] = self.gru04(att[0], net[0], inp[0], enc, interp(net[1], net[0]))
+        delta_disp = self.disp_head(net[0])
+        mask = _conv(self.mask[2], [_conv(self.mask[0], [net[0]], "relu")], "relu", alpha=0.25)
         return net, mask, delta_disp
 
     def _forward_fast(self, net, inp, corr, disp, att):
