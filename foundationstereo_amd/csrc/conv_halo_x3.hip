@@ -52,9 +52,48 @@ struct HaloArgs {
   int nrt, nct, npix, nco;         // row tiles, col tiles, pixel tiles (B*nrt*nct), cout tiles
   int nsplit, kpc;                 // split-K factor, channel chunks per split
   float* ws;                       // [nsplit][B][Cout][H*W] partial sums when nsplit > 1
+  // SelectiveConvGRU gate epilogues (act 3..5), core/update.py:83-95,117; all (B, gHd, H, W)
+  // except gatt (B, 1, H, W)
+  const float* gh;                 // hidden state h
+  float* gz;                       // z = sigmoid(z_pre): written by act 3, read by act 4 / 5
+  const float* gatt;               // att
+  float* grh;                      // sigmoid(r_pre) * h, written by act 3
+  int gHd;
 };
 
 __device__ __forceinline__ float gelu_erf_h(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float sigm_h(float x) { return 1.f / (1.f + expf(-x)); }
+
+// Final value of output channel co at (b, hw) from the raw conv sum v (already x wscale).
+//  act 0/1/2: out[b, co0+co] = res + gamma * alpha * act(v + bias)      (none / ReLU / GELU-erf)
+//  act 3 (convz|convr):  co <  Hd: z[b,co] = sigmoid(v + bias);
+//                        co >= Hd: rh[b,co-Hd] = sigmoid(v + bias) * h[b,co-Hd]
+//  act 4 (small convq):  out[b,co0+co] = ((1-z)h + z tanh(v + bias)) * att
+//  act 5 (large convq):  out[b,co0+co] += ((1-z)h + z tanh(v + bias)) * (1 - att)
+__device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, int b, int hw, int HW) {
+  if (a.bias) v += a.bias[co];
+  if (a.act >= 3) {
+    const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
+    if (a.act == 3) {
+      const float sg = sigm_h(v);
+      if (co < a.gHd) a.gz[g] = sg;
+      else a.grh[g] = sg * a.gh[g];
+      return;
+    }
+    const float z = a.gz[g], hv = a.gh[g], at = a.gatt[static_cast<size_t>(b) * HW + hw];
+    const float hn = (1.f - z) * hv + z * tanhf(v);
+    float* o = a.out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+    if (a.act == 4) *o = hn * at;
+    else *o = *o + hn * (1.f - at);
+    return;
+  }
+  if (a.act == 1) v = fmaxf(v, 0.f);
+  else if (a.act == 2) v = gelu_erf_h(v);
+  v *= a.alpha;
+  if (a.gamma) v *= a.gamma[co];
+  if (a.res) v += a.res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
+  a.out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw] = v;
+}
 
 // ---------------------------------------------------------------- shared pieces
 
@@ -192,24 +231,13 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
         }
       continue;
     }
-    float* ob = a.out + t.b * a.out_bstride + hw;
-    const float* rbp = a.res ? a.res + t.b * a.res_bstride + hw : nullptr;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-        if (co >= a.Cout) continue;
-        float v = acc[i][j][r] * a.wscale;
-        if (a.bias) v += a.bias[co];
-        if (a.act == 1) v = fmaxf(v, 0.f);
-        else if (a.act == 2) v = gelu_erf_h(v);
-        v *= a.alpha;
-        if (a.gamma) v *= a.gamma[co];
-        if (rbp) v += rbp[static_cast<size_t>(co) * HW];
-        ob[static_cast<size_t>(a.co0 + co) * HW] = v;
+        if (co < a.Cout) store_out(a, acc[i][j][r] * a.wscale, co, t.b, hw, HW);
       }
-    }
   }
 }
 
@@ -439,17 +467,11 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
   const int b = static_cast<int>(i / (HW * a.Cout));
   float v = 0.f;
   for (int sp = 0; sp < a.nsplit; ++sp) v += a.ws[sp * n + i];
-  if (a.bias) v += a.bias[co];
-  if (a.act == 1) v = fmaxf(v, 0.f);
-  else if (a.act == 2) v = gelu_erf_h(v);
-  v *= a.alpha;
-  if (a.gamma) v *= a.gamma[co];
-  if (a.res) v += a.res[b * a.res_bstride + co * HW + hw];
-  a.out[b * a.out_bstride + (a.co0 + co) * HW + hw] = v;
+  store_out(a, v, co, b, hw, static_cast<int>(HW));
 }
 
-// Vector form (H*W % 4 == 0): one (b, co) plane per blockIdx.y, float4 per thread,
-// all nsplit partial loads in flight before the ordered sum.
+// Vector form (H*W % 4 == 0): one (b, co) plane per blockIdx.y, float4 partial loads, all
+// nsplit of them in flight before the ordered sum.
 __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
   const int HW = a.H * a.W;
   const int hw = (blockIdx.x * 256 + threadIdx.x) * 4;
@@ -465,21 +487,25 @@ __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
 #pragma unroll
   for (int sp = 1; sp < 8; ++sp)
     if (sp < a.nsplit) { v.x += p[sp].x; v.y += p[sp].y; v.z += p[sp].z; v.w += p[sp].w; }
-  const float bb = a.bias ? a.bias[co] : 0.f;
-  float r[4] = {v.x + bb, v.y + bb, v.z + bb, v.w + bb};
+  if (a.act <= 2 && !a.res) {      // plain epilogue: vector store
+    const float bb = a.bias ? a.bias[co] : 0.f;
+    const float gg = a.gamma ? a.gamma[co] : 1.f;
+    float r[4] = {v.x + bb, v.y + bb, v.z + bb, v.w + bb};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (a.act == 1) r[k] = fmaxf(r[k], 0.f);
-    else if (a.act == 2) r[k] = gelu_erf_h(r[k]);
-    r[k] *= a.alpha;
-    if (a.gamma) r[k] *= a.gamma[co];
+    for (int k = 0; k < 4; ++k) {
+      if (a.act == 1) r[k] = fmaxf(r[k], 0.f);
+      else if (a.act == 2) r[k] = gelu_erf_h(r[k]);
+      r[k] *= a.alpha;
+      if (a.gamma) r[k] *= gg;
+    }
+    *reinterpret_cast<float4*>(a.out + b * a.out_bstride + static_cast<size_t>(a.co0 + co) * HW + hw) =
+        make_float4(r[0], r[1], r[2], r[3]);
+    return;
   }
-  if (a.res) {
-    const float4 q = *reinterpret_cast<const float4*>(a.res + b * a.res_bstride + static_cast<size_t>(co) * HW + hw);
-    r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
-  }
-  *reinterpret_cast<float4*>(a.out + b * a.out_bstride + static_cast<size_t>(a.co0 + co) * HW + hw) =
-      make_float4(r[0], r[1], r[2], r[3]);
+  store_out(a, v.x, co, b, hw, HW);
+  store_out(a, v.y, co, b, hw + 1, HW);
+  store_out(a, v.z, co, b, hw + 2, HW);
+  store_out(a, v.w, co, b, hw + 3, HW);
 }
 
 template <int KS, int BM, int TR, int WM>
@@ -516,26 +542,26 @@ int launch_halo(HaloArgs a, hipStream_t s) {
 
 using namespace fsmi;
 
-extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
-                                   const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
-                                   const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
-                                   int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
-                                   long long ws_floats, void* stream) {
-  FSMI_CHECK_ARG(seg_ptr && seg_ch && seg_ctot && whi && wlo && out, "fsmi_conv2d_halo_x3: null pointer");
-  FSMI_CHECK_ARG(nseg >= 1 && nseg <= kHMaxSeg, "fsmi_conv2d_halo_x3: 1..%d segments, got %d", kHMaxSeg, nseg);
-  FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "fsmi_conv2d_halo_x3: bad shape");
-  FSMI_CHECK_ARG(KS == 1 || KS == 3, "fsmi_conv2d_halo_x3: kernel %d unsupported (1, 3)", KS);
-  FSMI_CHECK_ARG(act >= 0 && act <= 2, "fsmi_conv2d_halo_x3: act %d", act);
-  FSMI_CHECK_ARG(co0 >= 0 && co0 + Cout <= out_ctot, "fsmi_conv2d_halo_x3: output slice outside the tensor");
-  HaloArgs a{};
+namespace {
+
+// Shared host side of both entry points: validates, fills HaloArgs (gate fields preset by the
+// caller), picks tiles and split-K, launches.
+int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot,
+             int nseg, const void* whi, const void* wlo, int wexp, const float* bias, float* out, int out_ctot,
+             int co0, int B, int Cout, int KS, int H, int W, int cfg, int nsplit, float* ws, long long ws_floats,
+             void* stream) {
+  FSMI_CHECK_ARG(seg_ptr && seg_ch && seg_ctot && whi && wlo, "%s: null pointer", what);
+  FSMI_CHECK_ARG(nseg >= 1 && nseg <= kHMaxSeg, "%s: 1..%d segments, got %d", what, kHMaxSeg, nseg);
+  FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "%s: bad shape", what);
+  FSMI_CHECK_ARG(KS == 1 || KS == 3, "%s: kernel %d unsupported (1, 3)", what, KS);
+  FSMI_CHECK_ARG(a.act == 3 || (out && co0 >= 0 && co0 + Cout <= out_ctot), "%s: output slice outside the tensor",
+                 what);
   int cin = 0;
   const long long HW = static_cast<long long>(H) * W;
   for (int i = 0; i < nseg; ++i) {
-    FSMI_CHECK_ARG(seg_ptr[i] && seg_ch[i] > 0 && seg_ctot[i] >= seg_ch[i], "fsmi_conv2d_halo_x3: bad segment %d",
-                   i);
+    FSMI_CHECK_ARG(seg_ptr[i] && seg_ch[i] > 0 && seg_ctot[i] >= seg_ch[i], "%s: bad segment %d", what, i);
     FSMI_CHECK_ARG(i == nseg - 1 || seg_ch[i] % 8 == 0,
-                   "fsmi_conv2d_halo_x3: inner segments must be multiples of 8 channels (segment %d: %d)", i,
-                   seg_ch[i]);
+                   "%s: inner segments must be multiples of 8 channels (segment %d: %d)", what, i, seg_ch[i]);
     a.seg_ptr[i] = seg_ptr[i];
     a.seg_bstride[i] = static_cast<long long>(seg_ctot[i]) * HW;
     cin += seg_ch[i];
@@ -548,9 +574,6 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
   a.wlo = static_cast<const _Float16*>(wlo);
   a.wscale = ldexpf(1.f, -wexp);
   a.bias = bias;
-  a.gamma = gamma;
-  a.res = res;
-  a.res_bstride = static_cast<long long>(res_ctot) * HW;
   a.out = out;
   a.out_bstride = static_cast<long long>(out_ctot) * HW;
   a.co0 = co0;
@@ -559,18 +582,15 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
   a.B = B;
   a.H = H;
   a.W = W;
-  a.act = act;
-  a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_CONV2D, s);
   // default tiles, measured per layer shape (tools/conv_bench.py --all-cfg): 3x3 layers run best
   // with register-resident weights (128 couts, or 64 for narrow outputs), 1x1 layers -- one tap
   // per chunk, so the per-tap LDS barrier is no cost -- with LDS weights and 128 couts
   if (cfg < 0) cfg = KS == 3 ? (Cout > 64 ? 3 : 2) : (Cout > 64 ? 1 : 0);
-  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 3, "fsmi_conv2d_halo_x3: cfg %d (0..3)", cfg);
+  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 3, "%s: cfg %d (0..3)", what, cfg);
   if (cfg & 1) tile_counts<3, 128, 4, 2>(a);      // odd cfgs: 128 couts x 4x32 px; even: 64 x 8x32
   else tile_counts<3, 64, 8, 1>(a);
-  // split-K when the output tiles alone cannot fill 256 CUs x 2 resident blocks
   const int nck = a.CinP / HKC;
   const long long per_split = static_cast<long long>(B) * Cout * H * W;
   if (nsplit < 0) {
@@ -587,7 +607,7 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
   a.kpc = (nck + nsplit - 1) / nsplit;
   a.nsplit = (nck + a.kpc - 1) / a.kpc;                    // no empty splits
   FSMI_CHECK_ARG(a.nsplit == 1 || (ws && per_split * a.nsplit <= ws_floats),
-                 "fsmi_conv2d_halo_x3: split-K %d needs %lld workspace floats", a.nsplit, per_split * a.nsplit);
+                 "%s: split-K %d needs %lld workspace floats", what, a.nsplit, per_split * a.nsplit);
   a.ws = ws;
   if (KS == 3) {
     switch (cfg) {
@@ -603,4 +623,44 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
     case 2: return launch_halo<1, 64, 8, 1, true>(a, s);
     default: return launch_halo<1, 128, 4, 2, true>(a, s);
   }
+}
+
+}  // namespace
+
+extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
+                                   const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
+                                   const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
+                                   int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
+                                   long long ws_floats, void* stream) {
+  FSMI_CHECK_ARG(out, "fsmi_conv2d_halo_x3: null output");
+  FSMI_CHECK_ARG(act >= 0 && act <= 2, "fsmi_conv2d_halo_x3: act %d", act);
+  HaloArgs a{};
+  a.act = act;
+  a.alpha = alpha;
+  a.gamma = gamma;
+  a.res = res;
+  a.res_bstride = static_cast<long long>(res_ctot) * H * W;
+  return run_halo(a, "fsmi_conv2d_halo_x3", seg_ptr, seg_ch, seg_ctot, nseg, whi, wlo, wexp, bias, out, out_ctot,
+                  co0, B, Cout, KS, H, W, cfg, nsplit, ws, ws_floats, stream);
+}
+
+extern "C" int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot,
+                                        int nseg, const void* whi, const void* wlo, int wexp, const float* bias,
+                                        int mode, const float* h, float* z, const float* att, float* rh, int Hd,
+                                        float* out, int out_ctot, int co0, int B, int Cout, int KS, int H, int W,
+                                        int cfg, int nsplit, float* ws, long long ws_floats, void* stream) {
+  FSMI_CHECK_ARG(mode >= 0 && mode <= 2, "fsmi_conv2d_halo_x3_gate: mode %d (0 zr, 1 small, 2 large)", mode);
+  FSMI_CHECK_ARG(h && z && Hd > 0, "fsmi_conv2d_halo_x3_gate: null h / z");
+  FSMI_CHECK_ARG(mode != 0 || (rh && Cout == 2 * Hd), "fsmi_conv2d_halo_x3_gate: zr needs rh and Cout == 2*Hd");
+  FSMI_CHECK_ARG(mode == 0 || (att && out && Cout == Hd), "fsmi_conv2d_halo_x3_gate: blend needs att, out, Cout == Hd");
+  HaloArgs a{};
+  a.act = 3 + mode;
+  a.alpha = 1.f;
+  a.gh = h;
+  a.gz = z;
+  a.gatt = att;
+  a.grh = rh;
+  a.gHd = Hd;
+  return run_halo(a, "fsmi_conv2d_halo_x3_gate", seg_ptr, seg_ch, seg_ctot, nseg, whi, wlo, wexp, bias, out,
+                  out_ctot, co0, B, Cout, KS, H, W, cfg, nsplit, ws, ws_floats, stream);
 }

@@ -221,7 +221,7 @@ class FoundationStereo(nn.Module):
         disp = init_disp.float()
         disp_preds = []
         disp_up = None
-        overlap = not mp and _update._fast(disp)
+        overlap = _update.OVERLAP and not mp and _update._fast(disp)
         for itr in range(iters):
             disp = disp.detach()
             if overlap:    # lookup + motion encoder on a side stream beside gru16/gru08 (same math)

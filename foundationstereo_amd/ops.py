@@ -326,6 +326,44 @@ def _segments(segs):
     return norm, (ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), chs, tots, ptrs), sum(n for _, _, n in norm)
 
 
+_GATE_MODE = {"zr": 0, "blend_small": 1, "blend_large": 2}
+
+
+def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Tensor = None, rh: Tensor = None,
+                out: Tensor = None, nsplit: int = -1, cfg: int = -1):
+    """Halo conv with a SelectiveConvGRU gate epilogue (``fsmi_conv2d_halo_x3_gate``).
+
+    ``mode`` "zr": ``pk`` = [convz; convr] stacked; writes ``z = sigmoid(.)`` and ``rh = sigmoid(r)*h``.
+    "blend_small": ``out = ((1-z)h + z*tanh(convq)) * att``; "blend_large": ``out += (...) * (1-att)``
+    (core/update.py:88-95,117)."""
+    assert pk.mode == "halo", "conv2d_gate: needs a PackedConv(mode='halo')"
+    norm, (pp, chs, tots, keep), cin = _segments(segs)
+    t0 = norm[0][0]
+    B, _, H, W = t0.shape
+    Hd = h.shape[1]
+    m = _GATE_MODE[mode]
+    extra = [x for x in (bias, h, z, att, rh, out) if x is not None]
+    _check("conv2d_gate", *[t for t, _, _ in norm], *extra)
+    assert cin == pk.cin, f"conv2d_gate: {cin} input channels for a conv packed with {pk.cin}"
+    for x in (h, z, att, rh, out):
+        assert x is None or (x.is_contiguous() and x.shape[0] == B and x.shape[2:] == (H, W)), \
+            "conv2d_gate: shape mismatch"
+    if m == 0:
+        assert pk.cout == 2 * Hd and rh is not None
+    else:
+        assert pk.cout == Hd and att is not None and out is not None
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * cin * pk.cout * pk.k * pk.k * B * H * W
+    stream = _stream(t0)
+    ws = _split_workspace(t0.device, stream, 8 * B * pk.cout * H * W)
+    _lib.check(_lib.load().fsmi_conv2d_halo_x3_gate(
+        pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, _p(bias), m, _p(h), _p(z),
+        _p(att) if att is not None else None, _p(rh) if rh is not None else None, Hd,
+        _p(out) if out is not None else None, out.shape[1] if out is not None else 0, 0, B, pk.cout, pk.k, H, W,
+        cfg, nsplit, _p(ws), ws.numel(), stream), "conv2d_gate")
+    del keep
+
+
 _SPLIT_WS = {}
 
 

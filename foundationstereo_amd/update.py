@@ -24,7 +24,12 @@ import torch.nn.functional as F
 from . import ops
 from .submodule import EdgeNextConvEncoder
 
+import os
+
 CONV_ENGINE = "fsmi"
+# A/B knobs (default on): motion path on a side stream; GRU gates in the conv epilogues
+OVERLAP = os.environ.get("FSMI_OVERLAP", "1") != "0"
+FUSED_GATES = os.environ.get("FSMI_FUSED_GATES", "1") != "0"
 
 
 def _fast(x) -> bool:
@@ -208,12 +213,24 @@ class SelectiveConvGRU(nn.Module):
         if _fast(h):
             xc = _conv(self.conv0[0], list(x), "relu")              # cat(x) as input segments
             hx = _conv(self.conv1[0], [xc, h], "relu")
-            zr_s = self.small_gru.zr_fast(hx)
-            zr_l = self.large_gru.zr_fast(hx)
-            qs_in, ql_in = ops.gru_reset(zr_s, zr_l, h, xc)
-            q_s = _conv(self.small_gru.convq, [qs_in])
-            q_l = _conv(self.large_gru.convq, [ql_in])
-            return ops.gru_blend(zr_s, zr_l, q_s, q_l, h, att.float())
+            # gates in the conv epilogues: z / r*h from the stacked zr convs, then each convq reads
+            # [r*h, x] as two segments and blends straight into the new state
+            if not FUSED_GATES:
+                zr_s = self.small_gru.zr_fast(hx)
+                zr_l = self.large_gru.zr_fast(hx)
+                qs_in, ql_in = ops.gru_reset(zr_s, zr_l, h, xc)
+                q_s = _conv(self.small_gru.convq, [qs_in])
+                q_l = _conv(self.large_gru.convq, [ql_in])
+                return ops.gru_blend(zr_s, zr_l, q_s, q_l, h, att.float())
+            att = att.float().contiguous()
+            out = torch.empty_like(h)
+            for gru, mode in ((self.small_gru, "blend_small"), (self.large_gru, "blend_large")):
+                z, rh = torch.empty_like(h), torch.empty_like(h)
+                pk, b = _packed(gru.convz, gru.convr)
+                ops.conv2d_gate([hx], pk, b, "zr", h=h, z=z, rh=rh)
+                pk, b = _packed(gru.convq)
+                ops.conv2d_gate([rh, xc], pk, b, mode, h=h, z=z, att=att, out=out)
+            return out
         x = torch.cat(x, dim=1) if len(x) > 1 else x[0]
         x = self.conv0(x)
         hx = self.conv1(torch.cat([x, h], dim=1))

@@ -182,6 +182,20 @@ int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const in
                         int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
                         long long ws_floats, void* stream);
 
+/* The same halo conv with a SelectiveConvGRU gate as its epilogue (replaces
+ * the gate elementwise passes of core/update.py:88-95,117; Hd = hidden channels,
+ * h / z / rh / out (B,Hd,H,W), att (B,1,H,W), all written/read in place):
+ *   mode 0 (convz|convr stacked, Cout = 2Hd): z = sigmoid(conv[:Hd]),
+ *          rh = sigmoid(conv[Hd:]) * h   (rh then feeds convq as a segment beside x);
+ *   mode 1 (small GRU convq, Cout = Hd): out[:, co0:] = ((1-z)h + z tanh(conv)) * att;
+ *   mode 2 (large GRU convq):            out[:, co0:] += ((1-z)h + z tanh(conv)) * (1-att).
+ * conv includes the bias.  Other arguments as fsmi_conv2d_halo_x3. */
+int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
+                             const void* whi, const void* wlo, int wexp, const float* bias, int mode,
+                             const float* h, float* z, const float* att, float* rh, int Hd, float* out,
+                             int out_ctot, int co0, int B, int Cout, int KS, int H, int W, int cfg, int nsplit,
+                             float* ws, long long ws_floats, void* stream);
+
 /* ---- refinement-loop auxiliaries ---------------------------------------
  * fsmi_dwconv2d: depthwise KSxKS conv (KS in {3,5,7}, stride 1, zero pad KS/2)
  *   x, out (B,C,H,W); w (C,1,KS,KS); bias (C) or NULL.  Replaces the EdgeNeXt

@@ -288,6 +288,27 @@ def test_gru_gates_vs_torch(ops_mod):
     close(out, ref, atol=1e-6)
 
 
+@pytest.mark.parametrize("HW", [(24, 40), (13, 21)])
+def test_selective_gru_fused_vs_oracle(ops_mod, HW):
+    """SelectiveConvGRU with the gates in the conv epilogues (zr -> z, r*h; convq -> blend) vs the
+    oracle's unfused restatement (core/update.py:83-119).  Small maps take split-K, so both reduce
+    kernels (float4 at 24x40, scalar at 13x21) run the gate epilogues too."""
+    from foundationstereo_amd.update import SelectiveConvGRU
+    H, W = HW
+    B, Hd, Ci = 2, 32, 48
+    mod = SelectiveConvGRU(Hd, Ci + 16)
+    synth.init_module_(mod, seed=401)
+    mod = mod.to(DEV).eval()
+    h = synth.normal(402, (B, Hd, H, W))
+    x1, x2 = synth.normal(403, (B, Ci, H, W)), synth.normal(404, (B, 16, H, W))
+    att = synth.uniform(405, (B, 1, H, W), 0.0, 1.0)
+    with torch.no_grad():
+        out = mod(g(att), g(h), g(x1), g(x2))
+    P = {"m." + k: v.cpu() for k, v in mod.state_dict().items()}
+    ref = oracle.stereo_oracle.selective_gru(P, "m", t(att), t(h), t(x1), t(x2))
+    close(out, ref, atol=2e-5)
+
+
 def test_update_step_golden(ops_mod):
     gd = load_golden("update_step")
     from foundationstereo_amd.update import BasicSelectiveMultiUpdateBlock
