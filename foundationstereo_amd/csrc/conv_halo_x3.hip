@@ -585,12 +585,20 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_CONV2D, s);
   // default tiles, measured per layer shape (tools/conv_bench.py --all-cfg): 3x3 layers run best
-  // with register-resident weights (128 couts, or 64 for narrow outputs), 1x1 layers -- one tap
-  // per chunk, so the per-tap LDS barrier is no cost -- with LDS weights and 128 couts
-  if (cfg < 0) cfg = KS == 3 ? (Cout > 64 ? 3 : 2) : (Cout > 64 ? 1 : 0);
-  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 3, "%s: cfg %d (0..3)", what, cfg);
-  if (cfg & 1) tile_counts<3, 128, 4, 2>(a);      // odd cfgs: 128 couts x 4x32 px; even: 64 x 8x32
-  else tile_counts<3, 64, 8, 1>(a);
+  // with register-resident weights and two pixel fragments per wave (cfg 3; cfg 2 / 5 for narrow
+  // outputs); 1x1 layers -- one tap per chunk, too little MFMA work to cover a load issued a
+  // chunk ahead -- with one fragment per wave, which buys a third resident wave per SIMD (cfg 4)
+  if (cfg < 0) {
+    if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
+    else cfg = Cout > 64 ? 4 : 5;
+  }
+  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 5, "%s: cfg %d (0..5)", what, cfg);
+  switch (cfg) {                                  // tile = couts x (rows x 32 px)
+    case 0: case 2: tile_counts<3, 64, 8, 1>(a); break;
+    case 1: case 3: tile_counts<3, 128, 4, 2>(a); break;
+    case 4: tile_counts<3, 128, 2, 2>(a); break;
+    default: tile_counts<3, 64, 4, 1>(a); break;
+  }
   const int nck = a.CinP / HKC;
   const long long per_split = static_cast<long long>(B) * Cout * H * W;
   if (nsplit < 0) {
@@ -614,14 +622,18 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
       case 0: return launch_halo<3, 64, 8, 1, false>(a, s);
       case 1: return launch_halo<3, 128, 4, 2, false>(a, s);
       case 2: return launch_halo<3, 64, 8, 1, true>(a, s);
-      default: return launch_halo<3, 128, 4, 2, true>(a, s);
+      case 3: return launch_halo<3, 128, 4, 2, true>(a, s);
+      case 4: return launch_halo<3, 128, 2, 2, true>(a, s);
+      default: return launch_halo<3, 64, 4, 1, true>(a, s);
     }
   }
   switch (cfg) {
     case 0: return launch_halo<1, 64, 8, 1, false>(a, s);
     case 1: return launch_halo<1, 128, 4, 2, false>(a, s);
     case 2: return launch_halo<1, 64, 8, 1, true>(a, s);
-    default: return launch_halo<1, 128, 4, 2, true>(a, s);
+    case 3: return launch_halo<1, 128, 4, 2, true>(a, s);
+    case 4: return launch_halo<1, 128, 2, 2, true>(a, s);
+    default: return launch_halo<1, 64, 4, 1, true>(a, s);
   }
 }
 

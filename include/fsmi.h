@@ -169,7 +169,9 @@ int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* se
  * 32-channel chunk and runs all taps from LDS.  Inner segments must hold a
  * multiple of 8 channels.  cfg 0: 64 couts x 8x32 px, 1: 128 couts x 4x32 px
  * (weights staged per tap through LDS); 2 / 3: the same tiles with each wave's
- * weight fragments loaded into registers one tap ahead; -1: measured default.
+ * weight fragments loaded into registers one tap ahead; 4: 128 couts x 2x32 px,
+ * 5: 64 couts x 4x32 px (registers, one pixel fragment per wave: 3 waves/SIMD);
+ * -1: measured default.
  * nsplit: split-K over 32-channel chunks (<0: auto, sized to fill the chip);
  * partial sums go to ws (nsplit*B*Cout*H*W floats, ws_floats available) and
  * a second kernel sums them in split order (deterministic) and applies the

@@ -148,10 +148,10 @@ def test_conv2d_mfma_vs_torch(ops_mod, mode, cfg, k, cout, act):
 
 @pytest.mark.parametrize("HW", [(19, 45), (12, 40)])
 @pytest.mark.parametrize("nsplit", [1, 2])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (3, 136, None), (1, 129, "relu")])
 def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
-    """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2/3 in registers): 2 segments (16 channels + a 29-channel slice -> 2 channel
+    """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2-5 in registers): 2 segments (16 channels + a 29-channel slice -> 2 channel
     chunks, ragged last chunk), ragged row/column tiles (19x45; 12x40 takes the float4 split-K
     reduce), ragged couts, output slice, every epilogue term, with and without split-K; vs fp64
     torch.  Same 2e-5 abs + 1e-5 rel tolerance as the im2col kernels."""

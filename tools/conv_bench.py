@@ -76,7 +76,7 @@ for name, cin, cout, k, H, W in SHAPES:
     for ns in a.nsplit:
         row[f"split{ns}_us"] = round(timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", nsplit=ns)), 1)
     if a.all_cfg:
-        for c in range(4):
+        for c in range(6 if a.mode == "halo" else 4):
             row[f"cfg{c}_us"] = round(timeit(lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=c)), 1)
     rows.append(row)
     tot_m += t_m
