@@ -49,9 +49,14 @@ struct HaloArgs {
   long long out_bstride;
   int co0, Cout, CoutP, B, H, W, act;
   float alpha;
-  int nrt, nct, npix, nco;         // row tiles, col tiles, pixel tiles (B*nrt*nct), cout tiles
-  int nsplit, kpc;                 // split-K factor, channel chunks per split
-  float* ws;                       // [nsplit][B][Cout][H*W] partial sums when nsplit > 1
+  int res_pre;                     // residual added before the activation (ResNet block tail)
+  // 3D: NCDHW tensors with D depth planes; a KD x KS x KS kernel is the sum over kd of 2D
+  // convs on plane d + kd - PDD.  2D: D = KD = 1.
+  int D, KD, PDD;
+  long long cstride;               // channel stride = D*H*W
+  int nrt, nct, npix, nco;         // row tiles, col tiles, pixel tiles (B*D*nrt*nct), cout tiles
+  int nsplit, kpc;                 // split-K factor, (kd, channel chunk) pairs per split
+  float* ws;                       // [nsplit][B][Cout][D*H*W] partial sums when nsplit > 1
   // SelectiveConvGRU gate epilogues (act 3..5), core/update.py:83-95,117; all (B, gHd, H, W)
   // except gatt (B, 1, H, W)
   const float* gh;                 // hidden state h
@@ -64,15 +69,21 @@ struct HaloArgs {
 __device__ __forceinline__ float gelu_erf_h(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float sigm_h(float x) { return 1.f / (1.f + expf(-x)); }
 
-// Final value of output channel co at (b, hw) from the raw conv sum v (already x wscale).
-//  act 0/1/2: out[b, co0+co] = res + gamma * alpha * act(v + bias)      (none / ReLU / GELU-erf)
+// Final value of output channel co at (b, sp) -- sp = d*H*W + h*W + w -- from the raw conv sum v
+// (already x wscale).
+//  act 0/1/2/6: out[b, co0+co] = res + gamma * alpha * act(v + bias)   (none / ReLU / GELU-erf /
+//               LeakyReLU 0.01); with res_pre: gamma * alpha * act(v + bias + res)
 //  act 3 (convz|convr):  co <  Hd: z[b,co] = sigmoid(v + bias);
 //                        co >= Hd: rh[b,co-Hd] = sigmoid(v + bias) * h[b,co-Hd]
 //  act 4 (small convq):  out[b,co0+co] = ((1-z)h + z tanh(v + bias)) * att
 //  act 5 (large convq):  out[b,co0+co] += ((1-z)h + z tanh(v + bias)) * (1 - att)
-__device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, int b, int hw, int HW) {
+// RESPRE: compile the res_pre (ResNet tail) path; the 2D conv kernels instantiate without it --
+// with the branch present their epilogue needs ~100 more VGPRs (occupancy 2 -> 1).
+template <bool RESPRE = true>
+__device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, int b, long long hw) {
+  const long long HW = a.cstride;
   if (a.bias) v += a.bias[co];
-  if (a.act >= 3) {
+  if (a.act >= 3 && a.act <= 5) {
     const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
     if (a.act == 3) {
       const float sg = sigm_h(v);
@@ -87,12 +98,19 @@ __device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, in
     else *o = *o + hn * (1.f - at);
     return;
   }
+  float* o = a.out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+  if (RESPRE && a.res_pre) {       // ResNet tail: act(v + bias + res)
+    v += a.res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
+    *o = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v);
+    return;
+  }
   if (a.act == 1) v = fmaxf(v, 0.f);
   else if (a.act == 2) v = gelu_erf_h(v);
+  else if (a.act == 6) v = v >= 0.f ? v : 0.01f * v;
   v *= a.alpha;
   if (a.gamma) v *= a.gamma[co];
   if (a.res) v += a.res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
-  a.out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw] = v;
+  *o = v;
 }
 
 // ---------------------------------------------------------------- shared pieces
@@ -121,9 +139,12 @@ struct HaloStage {
     }
   }
 
-  __device__ __forceinline__ void load(const HaloArgs& a, int b, int cc) {
-    const int HW = a.H * a.W;
+  // chunk cc of depth plane d (zeros outside [0, D))
+  __device__ __forceinline__ void load(const HaloArgs& a, int b, int cc, int d = 0) {
+    const long long HW = a.cstride;
     const bool full = (cc + 1) * HKC <= a.Cin;     // block-uniform: only the last chunk is ragged
+    const bool plane_ok = d >= 0 && d < a.D;
+    const long long poff = static_cast<long long>(min(max(d, 0), a.D - 1)) * a.H * a.W;
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u) {
       const int g = desc[u] & 3, pix = desc[u] >> 3;
@@ -141,8 +162,8 @@ struct HaloStage {
         sb = in_q ? a.seg_bstride[q] : sb;
         base = in_q ? a.seg_end[q - 1] : base;
       }
-      const float* src = sp + b * sb + static_cast<long long>(cic - base) * HW + pix;
-      const bool ok = desc[u] & 4;
+      const float* src = sp + b * sb + static_cast<long long>(cic - base) * HW + poff + pix;
+      const bool ok = (desc[u] & 4) && plane_ok;
       f32x8 v;
       if (full) {
 #pragma unroll
@@ -176,11 +197,11 @@ struct HaloStage {
 };
 
 struct TileCoord {
-  int m0, b, r0, c0, split;
+  int m0, b, d0, r0, c0, split;
 };
 
 // cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
-template <int BM, int TR>
+template <int BM, int TR, bool D3>
 __device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
   const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
   const int cs = item / a.npix;                    // (cout tile, split) pair
@@ -189,8 +210,11 @@ __device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
   TileCoord t;
   t.split = cs - ctile * a.nsplit;
   t.m0 = ctile * BM;
-  t.b = ptile / (a.nrt * a.nct);
-  const int prem = ptile - t.b * a.nrt * a.nct;
+  const int per_plane = a.nrt * a.nct;
+  const int bd = ptile / per_plane;                // (image, depth plane)
+  t.b = D3 ? bd / a.D : bd;
+  t.d0 = D3 ? bd - t.b * a.D : 0;
+  const int prem = ptile - bd * per_plane;
   t.r0 = (prem / a.nct) * TR;
   t.c0 = (prem % a.nct) * 32;
   return t;
@@ -210,16 +234,16 @@ __device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM
 }
 
 // n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
-template <int TM, int TN>
+template <int TM, int TN, bool D3>
 __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], const TileCoord& t,
                                               int wm, int wn, int lane) {
   const int hsel = lane >> 5, rl = lane & 31;
-  const int HW = a.H * a.W;
+  const long long HW = a.cstride;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
     if (hh >= a.H || ww >= a.W) continue;
-    const int hw = hh * a.W + ww;
+    const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
     if (a.nsplit > 1) {            // raw partial sums; the split reduce applies the epilogue
       float* wp = a.ws + (static_cast<size_t>(t.split) * a.B + t.b) * a.Cout * HW + hw;
 #pragma unroll
@@ -236,14 +260,14 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-        if (co < a.Cout) store_out(a, acc[i][j][r] * a.wscale, co, t.b, hw, HW);
+        if (co < a.Cout) store_out<D3>(a, acc[i][j][r] * a.wscale, co, t.b, hw);
       }
   }
 }
 
 // ---------------------------------------------------------------- cfg 0/1: weights through LDS
 
-template <int KS, int BM, int TR, int WM>
+template <int KS, int BM, int TR, int WM, bool D3>
 __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
@@ -260,14 +284,16 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int hsel = lane >> 5, rl = lane & 31;
-  const TileCoord tc = decode_tile<BM, TR>(a);
+  const TileCoord tc = decode_tile<BM, TR, D3>(a);
   const int m0 = tc.m0;
   const int nck = a.CinP / HKC;
+  const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
 
   const bool w_full = m0 + BM <= a.CoutP;          // block-uniform: only the last cout tile is ragged
   uint4 rwh[W_PER_T], rwl[W_PER_T];
   auto load_w = [&](int cc, int tap) {
-    const size_t base = (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+    const size_t base = D3 ? (static_cast<size_t>((cc / nck) * NTAP + tap) * nck + cc % nck) * a.CoutP * HKC
+                           : (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
     const _Float16* ph = a.whi + base;
     const _Float16* pl = a.wlo + base;
     if (w_full) {
@@ -312,16 +338,20 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // split-K: this block reduces channel chunks [cc_begin, cc_end)
+  // split-K: this block reduces chunks [cc_begin, cc_end)
   const int cc_begin = tc.split * a.kpc;
-  const int cc_end = min(nck, cc_begin + a.kpc);
+  const int cc_end = min(nq, cc_begin + a.kpc);
   int step = 0;
   load_w(cc_begin, 0);
-  hs.load(a, tc.b, cc_begin);
+  if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
+  else hs.load(a, tc.b, cc_begin);
   for (int cc = cc_begin; cc < cc_end; ++cc) {
     __syncthreads();               // every wave is done with the previous chunk's halo
     hs.store(Xh, Xl, tid);
-    if (cc + 1 < cc_end) hs.load(a, tc.b, cc + 1);   // in flight during this chunk's taps
+    if (cc + 1 < cc_end) {
+      if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
+      else hs.load(a, tc.b, cc + 1);
+    }   // in flight during this chunk's taps
 #pragma unroll 1
     for (int tap = 0; tap < NTAP; ++tap, ++step) {
       const int buf = step & 1;
@@ -350,12 +380,12 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
       }
     }
   }
-  conv_epilogue<TM, TN>(a, acc, tc, wm, wn, lane);
+  conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane);
 }
 
 // ---------------------------------------------------------------- cfg 2/3: weights in registers
 
-template <int KS, int BM, int TR, int WM>
+template <int KS, int BM, int TR, int WM, bool D3>
 __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
@@ -367,8 +397,9 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int hsel = lane >> 5, rl = lane & 31;
-  const TileCoord tc = decode_tile<BM, TR>(a);
+  const TileCoord tc = decode_tile<BM, TR, D3>(a);
   const int nck = a.CinP / HKC;
+  const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
 
   // this lane's A-fragment rows (rows past Cout only feed outputs the epilogue drops:
   // clamped so every address is mapped, no zeroing needed)
@@ -378,7 +409,8 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   half8 wf[2][TM][2][2];           // [buffer][i][k half][hi, lo]
   auto load_wf = [&](auto buf_c, int cc, int tap) {
     constexpr int buf = decltype(buf_c)::value;
-    const size_t base = (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+    const size_t base = D3 ? (static_cast<size_t>((cc / nck) * NTAP + tap) * nck + cc % nck) * a.CoutP * HKC
+                           : (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -399,7 +431,7 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int cc_begin = tc.split * a.kpc;
-  const int cc_end = min(nck, cc_begin + a.kpc);
+  const int cc_end = min(nq, cc_begin + a.kpc);
   // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
   auto chunk = [&](auto par_c, int cc) {
     constexpr int P = decltype(par_c)::value;
@@ -436,11 +468,15 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   auto stage = [&](int cc) {
     __syncthreads();               // every wave is done with the previous chunk's halo
     hs.store(Xh, Xl, tid);
-    if (cc + 1 < cc_end) hs.load(a, tc.b, cc + 1);   // in flight during this chunk's taps
+    if (cc + 1 < cc_end) {
+      if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
+      else hs.load(a, tc.b, cc + 1);
+    }   // in flight during this chunk's taps
     __syncthreads();
   };
   load_wf(std::integral_constant<int, 0>(), cc_begin, 0);
-  hs.load(a, tc.b, cc_begin);
+  if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
+  else hs.load(a, tc.b, cc_begin);
   // chunks in pairs so every register-buffer index is static (parity 0, then 1)
   int cc = cc_begin;
   for (; cc + 1 < cc_end; cc += 2) {
@@ -453,41 +489,41 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
     stage(cc);
     chunk(std::integral_constant<int, 0>(), cc);
   }
-  conv_epilogue<TM, TN>(a, acc, tc, wm, wn, lane);
+  conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane);
 }
 
 // Sums the split-K partials in split order (deterministic) and applies the epilogue.
 __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
-  const long long HW = static_cast<long long>(a.H) * a.W;
-  const long long n = static_cast<long long>(a.B) * a.Cout * HW;
+  const long long SP = a.cstride;
+  const long long n = static_cast<long long>(a.B) * a.Cout * SP;
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= n) return;
-  const int hw = static_cast<int>(i % HW);
-  const int co = static_cast<int>((i / HW) % a.Cout);
-  const int b = static_cast<int>(i / (HW * a.Cout));
+  const long long sp = i % SP;
+  const int co = static_cast<int>((i / SP) % a.Cout);
+  const int b = static_cast<int>(i / (SP * a.Cout));
   float v = 0.f;
-  for (int sp = 0; sp < a.nsplit; ++sp) v += a.ws[sp * n + i];
-  store_out(a, v, co, b, hw, static_cast<int>(HW));
+  for (int k = 0; k < a.nsplit; ++k) v += a.ws[k * n + i];
+  store_out(a, v, co, b, sp);
 }
 
-// Vector form (H*W % 4 == 0): one (b, co) plane per blockIdx.y, float4 partial loads, all
+// Vector form (D*H*W % 4 == 0): one (b, co) channel per blockIdx.y, float4 partial loads, all
 // nsplit of them in flight before the ordered sum.
 __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
-  const int HW = a.H * a.W;
-  const int hw = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (hw >= HW) return;
+  const long long SP = a.cstride;
+  const long long hw = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (hw >= SP) return;
   const int plane = blockIdx.y, co = plane % a.Cout, b = plane / a.Cout;
-  const size_t n = static_cast<size_t>(a.B) * a.Cout * HW;
-  const float* src = a.ws + static_cast<size_t>(plane) * HW + hw;
+  const size_t n = static_cast<size_t>(a.B) * a.Cout * SP;
+  const float* src = a.ws + static_cast<size_t>(plane) * SP + hw;
   float4 p[8];
 #pragma unroll
-  for (int sp = 0; sp < 8; ++sp)
-    if (sp < a.nsplit) p[sp] = *reinterpret_cast<const float4*>(src + sp * n);
+  for (int k = 0; k < 8; ++k)
+    if (k < a.nsplit) p[k] = *reinterpret_cast<const float4*>(src + k * n);
   float4 v = p[0];
 #pragma unroll
-  for (int sp = 1; sp < 8; ++sp)
-    if (sp < a.nsplit) { v.x += p[sp].x; v.y += p[sp].y; v.z += p[sp].z; v.w += p[sp].w; }
-  if (a.act <= 2 && !a.res) {      // plain epilogue: vector store
+  for (int k = 1; k < 8; ++k)
+    if (k < a.nsplit) { v.x += p[k].x; v.y += p[k].y; v.z += p[k].z; v.w += p[k].w; }
+  if ((a.act <= 2 || a.act == 6) && !a.res) {      // plain epilogue: vector store
     const float bb = a.bias ? a.bias[co] : 0.f;
     const float gg = a.gamma ? a.gamma[co] : 1.f;
     float r[4] = {v.x + bb, v.y + bb, v.z + bb, v.w + bb};
@@ -495,41 +531,49 @@ __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
     for (int k = 0; k < 4; ++k) {
       if (a.act == 1) r[k] = fmaxf(r[k], 0.f);
       else if (a.act == 2) r[k] = gelu_erf_h(r[k]);
+      else if (a.act == 6) r[k] = r[k] >= 0.f ? r[k] : 0.01f * r[k];
       r[k] *= a.alpha;
       if (a.gamma) r[k] *= gg;
     }
-    *reinterpret_cast<float4*>(a.out + b * a.out_bstride + static_cast<size_t>(a.co0 + co) * HW + hw) =
+    *reinterpret_cast<float4*>(a.out + b * a.out_bstride + static_cast<size_t>(a.co0 + co) * SP + hw) =
         make_float4(r[0], r[1], r[2], r[3]);
     return;
   }
-  store_out(a, v.x, co, b, hw, HW);
-  store_out(a, v.y, co, b, hw + 1, HW);
-  store_out(a, v.z, co, b, hw + 2, HW);
-  store_out(a, v.w, co, b, hw + 3, HW);
+  store_out(a, v.x, co, b, hw);
+  store_out(a, v.y, co, b, hw + 1);
+  store_out(a, v.z, co, b, hw + 2);
+  store_out(a, v.w, co, b, hw + 3);
 }
 
 template <int KS, int BM, int TR, int WM>
 void tile_counts(HaloArgs& a) {
   a.nrt = (a.H + TR - 1) / TR;
   a.nct = (a.W + 31) / 32;
-  a.npix = a.B * a.nrt * a.nct;
+  a.npix = a.B * a.D * a.nrt * a.nct;
   a.nco = (a.Cout + BM - 1) / BM;
 }
 
 template <int KS, int BM, int TR, int WM, bool WREG>
 int launch_halo(HaloArgs a, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
-  if (WREG) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
+  const bool d3 = a.D > 1 || a.KD > 1;
+  if constexpr (WREG) {
+    if (d3) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, true>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, false>), dim3(grid), dim3(256), 0, s, a);
+  } else {
+    if (d3) hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, true>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, false>), dim3(grid), dim3(256), 0, s, a);
+  }
   if (a.nsplit > 1) {
-    const int HW = a.H * a.W;
-    const bool vec = HW % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
+    const long long SP = a.cstride;
+    const bool vec = SP % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
                      reinterpret_cast<uintptr_t>(a.ws) % 16 == 0 &&
                      (!a.res || reinterpret_cast<uintptr_t>(a.res) % 16 == 0);
     if (vec) {
-      hipLaunchKernelGGL(conv_split_reduce4_kernel, dim3((HW / 4 + 255) / 256, a.B * a.Cout), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(conv_split_reduce4_kernel, dim3(static_cast<unsigned>((SP / 4 + 255) / 256), a.B * a.Cout),
+                         dim3(256), 0, s, a);
     } else {
-      const long long n = static_cast<long long>(a.B) * a.Cout * HW;
+      const long long n = static_cast<long long>(a.B) * a.Cout * SP;
       hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
                          a);
     }
@@ -549,15 +593,20 @@ namespace {
 int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot,
              int nseg, const void* whi, const void* wlo, int wexp, const float* bias, float* out, int out_ctot,
              int co0, int B, int Cout, int KS, int H, int W, int cfg, int nsplit, float* ws, long long ws_floats,
-             void* stream) {
+             void* stream, int D = 1, int KD = 1) {
   FSMI_CHECK_ARG(seg_ptr && seg_ch && seg_ctot && whi && wlo, "%s: null pointer", what);
   FSMI_CHECK_ARG(nseg >= 1 && nseg <= kHMaxSeg, "%s: 1..%d segments, got %d", what, kHMaxSeg, nseg);
   FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "%s: bad shape", what);
   FSMI_CHECK_ARG(KS == 1 || KS == 3, "%s: kernel %d unsupported (1, 3)", what, KS);
+  FSMI_CHECK_ARG(D >= 1 && KD >= 1 && KD % 2 == 1, "%s: depth %d / depth kernel %d (odd)", what, D, KD);
   FSMI_CHECK_ARG(a.act == 3 || (out && co0 >= 0 && co0 + Cout <= out_ctot), "%s: output slice outside the tensor",
                  what);
   int cin = 0;
-  const long long HW = static_cast<long long>(H) * W;
+  const long long HW = static_cast<long long>(D) * H * W;     // channel stride
+  a.D = D;
+  a.KD = KD;
+  a.PDD = KD / 2;
+  a.cstride = HW;
   for (int i = 0; i < nseg; ++i) {
     FSMI_CHECK_ARG(seg_ptr[i] && seg_ch[i] > 0 && seg_ctot[i] >= seg_ch[i], "%s: bad segment %d", what, i);
     FSMI_CHECK_ARG(i == nseg - 1 || seg_ch[i] % 8 == 0,
@@ -589,18 +638,21 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   // outputs); 1x1 layers -- one tap per chunk, too little MFMA work to cover a load issued a
   // chunk ahead -- with one fragment per wave, which buys a third resident wave per SIMD (cfg 4)
   if (cfg < 0) {
-    if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
+    if (Cout <= 32) cfg = 6;
+    else if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
     else cfg = Cout > 64 ? 4 : 5;
   }
-  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 5, "%s: cfg %d (0..5)", what, cfg);
+  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 7, "%s: cfg %d (0..7)", what, cfg);
   switch (cfg) {                                  // tile = couts x (rows x 32 px)
     case 0: case 2: tile_counts<3, 64, 8, 1>(a); break;
     case 1: case 3: tile_counts<3, 128, 4, 2>(a); break;
     case 4: tile_counts<3, 128, 2, 2>(a); break;
-    default: tile_counts<3, 64, 4, 1>(a); break;
+    case 5: tile_counts<3, 64, 4, 1>(a); break;
+    case 6: tile_counts<3, 32, 8, 1>(a); break;
+    default: tile_counts<3, 32, 4, 1>(a); break;
   }
-  const int nck = a.CinP / HKC;
-  const long long per_split = static_cast<long long>(B) * Cout * H * W;
+  const int nck = KD * a.CinP / HKC;               // split-K runs over (kd, channel chunk) pairs
+  const long long per_split = static_cast<long long>(B) * Cout * HW;
   if (nsplit < 0) {
     // measured on the cfg2 loop layers (tools/conv_bench.py --nsplit): 3x3 layers are best
     // near ~1200 blocks (~2.3 rounds of the 512 resident slots), 1x1 layers -- a quarter of
@@ -624,7 +676,9 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
       case 2: return launch_halo<3, 64, 8, 1, true>(a, s);
       case 3: return launch_halo<3, 128, 4, 2, true>(a, s);
       case 4: return launch_halo<3, 128, 2, 2, true>(a, s);
-      default: return launch_halo<3, 64, 4, 1, true>(a, s);
+      case 5: return launch_halo<3, 64, 4, 1, true>(a, s);
+      case 6: return launch_halo<3, 32, 8, 1, true>(a, s);
+      default: return launch_halo<3, 32, 4, 1, true>(a, s);
     }
   }
   switch (cfg) {
@@ -633,7 +687,9 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     case 2: return launch_halo<1, 64, 8, 1, true>(a, s);
     case 3: return launch_halo<1, 128, 4, 2, true>(a, s);
     case 4: return launch_halo<1, 128, 2, 2, true>(a, s);
-    default: return launch_halo<1, 64, 4, 1, true>(a, s);
+    case 5: return launch_halo<1, 64, 4, 1, true>(a, s);
+    case 6: return launch_halo<1, 32, 8, 1, true>(a, s);
+    default: return launch_halo<1, 32, 4, 1, true>(a, s);
   }
 }
 
@@ -675,4 +731,22 @@ extern "C" int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* 
   a.gHd = Hd;
   return run_halo(a, "fsmi_conv2d_halo_x3_gate", seg_ptr, seg_ch, seg_ctot, nseg, whi, wlo, wexp, bias, out,
                   out_ctot, co0, B, Cout, KS, H, W, cfg, nsplit, ws, ws_floats, stream);
+}
+
+extern "C" int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wlo, int wexp,
+                                   const float* bias, const float* res, float* out, int B, int Cout, int D, int H,
+                                   int W, int KD, int KS, int act, int res_pre, int cfg, int nsplit, float* ws,
+                                   long long ws_floats, void* stream) {
+  FSMI_CHECK_ARG(x && out && Cin > 0, "fsmi_conv3d_halo_x3: null pointer / channels");
+  FSMI_CHECK_ARG(act == 0 || act == 1 || act == 6, "fsmi_conv3d_halo_x3: act %d (0 none, 1 ReLU, 6 LeakyReLU)", act);
+  HaloArgs a{};
+  a.act = act;
+  a.alpha = 1.f;
+  a.res = res;
+  a.res_pre = res_pre;
+  a.res_bstride = static_cast<long long>(Cout) * D * H * W;
+  const float* seg[1] = {x};
+  const int ch[1] = {Cin}, tot[1] = {Cin};
+  return run_halo(a, "fsmi_conv3d_halo_x3", seg, ch, tot, 1, whi, wlo, wexp, bias, out, Cout, 0, B, Cout, KS, H, W,
+                  cfg, nsplit, ws, ws_floats, stream, D, KD);
 }

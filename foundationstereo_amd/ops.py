@@ -285,23 +285,31 @@ class PackedConv:
 
     def __init__(self, *weights: Tensor, mode: str = "x3"):
         w = torch.cat([x.detach().float() for x in weights], 0)
-        self.cout, self.cin, self.k, kw = w.shape
+        if w.dim() == 5:                    # Conv3d (Cout, Cin, KD, KS, KS): taps kd-major
+            self.kd = w.shape[2]
+            w = w.permute(0, 1, 3, 4, 2)    # taps are packed as (kd, kh, kw) below
+        else:
+            self.kd = 1
+            w = w.unsqueeze(-1)
+        self.cout, self.cin, self.k, kw, _ = w.shape
         assert self.k == kw
         self.mode = mode
         assert mode in ("f32", "x3", "halo"), mode
         assert mode != "halo" or self.k in (1, 3), "halo conv: 1x1 or 3x3 only"
+        assert self.kd == 1 or mode == "halo", "3D weights: halo mode only"
         if mode == "f32":
-            self.wpk = pack_conv_weight(w)
+            self.wpk = pack_conv_weight(w[..., 0])
             return
         import math
         amax = float(w.abs().max())
         self.wexp = 0 if amax == 0 else -int(math.floor(math.log2(amax)))   # max |w| * 2^wexp in [1, 2)
         cinp = (self.cin + 31) // 32 * 32
         coutp = (self.cout + 31) // 32 * 32
-        ws = torch.zeros((coutp, cinp, self.k, self.k), device=w.device, dtype=torch.float32)
-        ws[:self.cout, :self.cin] = w * (2.0 ** self.wexp)
-        # [tap][cin chunk][cout][32]
-        ws = ws.permute(2, 3, 1, 0).reshape(self.k * self.k, cinp // 32, 32, coutp).permute(0, 1, 3, 2).contiguous()
+        ws = torch.zeros((coutp, cinp, self.kd, self.k, self.k), device=w.device, dtype=torch.float32)
+        ws[:self.cout, :self.cin] = w.permute(0, 1, 4, 2, 3) * (2.0 ** self.wexp)
+        # [tap = (kd, kh, kw)][cin chunk][cout][32]
+        ws = ws.permute(2, 3, 4, 1, 0).reshape(self.kd * self.k * self.k, cinp // 32, 32, coutp) \
+            .permute(0, 1, 3, 2).contiguous()
         hi = ws.half()
         lo = (ws - hi.float()).half()
         self.whi, self.wlo = hi.contiguous(), lo.contiguous()
@@ -324,6 +332,34 @@ def _segments(segs):
     chs = (ctypes.c_int * nseg)(*[n for _, _, n in norm])
     tots = (ctypes.c_int * nseg)(*[t.shape[1] for t, _, _ in norm])
     return norm, (ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_void_p)), chs, tots, ptrs), sum(n for _, _, n in norm)
+
+
+_ACT3D = {None: 0, "relu": 1, "leaky": 6}
+
+
+def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res_pre: bool = False,
+           cfg: int = -1, nsplit: int = -1) -> Tensor:
+    """Stride-1 'same' Conv3d (KD x K x K, K in {1, 3}, KD odd) on the halo split-precision
+    kernel (``fsmi_conv3d_halo_x3``); NCDHW in and out.  ``act`` None / "relu" / "leaky" (0.01);
+    ``res`` is added after the activation, or before it with ``res_pre`` (ResNet block tail)."""
+    assert pk.mode == "halo" and x.dim() == 5
+    _check("conv3d", x, *[t for t in (bias, res) if t is not None])
+    B, Cin, D, H, W = x.shape
+    assert Cin == pk.cin, f"conv3d: {Cin} input channels for a conv packed with {pk.cin}"
+    x = _c(x)
+    out = torch.empty((B, pk.cout, D, H, W), device=x.device, dtype=torch.float32)
+    if res is not None:
+        res = _c(res)
+        assert res.shape == out.shape
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * Cin * pk.cout * pk.kd * pk.k * pk.k * B * D * H * W
+    stream = _stream(x)
+    ws = _split_workspace(x.device, stream, 4 * B * pk.cout * D * H * W)
+    _lib.check(_lib.load().fsmi_conv3d_halo_x3(
+        _p(x), Cin, _p(pk.whi), _p(pk.wlo), pk.wexp, _p(bias) if bias is not None else None,
+        _p(res) if res is not None else None, _p(out), B, pk.cout, D, H, W, pk.kd, pk.k, _ACT3D[act],
+        1 if res_pre else 0, cfg, nsplit, _p(ws), ws.numel(), stream), "conv3d")
+    return out
 
 
 _GATE_MODE = {"zr": 0, "blend_small": 1, "blend_large": 2}

@@ -3,14 +3,19 @@
 Public names and module trees (hence ``state_dict`` keys) match the reference
 so ``core.foundation_stereo`` can star-import this module instead
 (SURVEY §8b).  The cost-volume functions, ``disparity_regression`` and
-``context_upsample`` run the hand-written gfx950 kernels of ``libfsmi.so``;
-dense convolutions stay on MIOpen through ``torch.nn``.
+``context_upsample`` run the hand-written gfx950 kernels of ``libfsmi.so``.
+Stride-1 3D conv blocks (``BasicConv``, ``Conv3dNormActReduced``,
+``ResnetBasicBlock3D``) run the halo split-precision conv kernel with the eval
+BatchNorm folded into the packed weights (``conv3d_bn_act``); strided / transposed
+3D convs and the 2D feature convs stay on MIOpen through ``torch.nn``.
 
 The disparity transformer's attention uses PyTorch SDPA in place of the
 reference's third-party ``flash_attn_func`` (core/submodule.py:224): same
 non-causal softmax(QK^T/sqrt(d))V math.
 """
 from __future__ import annotations
+
+import os
 
 import math
 
@@ -43,6 +48,49 @@ class LayerNorm2d(nn.LayerNorm):
         return y.permute(0, 3, 1, 2).contiguous()
 
 
+FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
+
+
+def _fast3d(x, conv, bn) -> bool:
+    """Stride-1 'same' Conv3d (+ eval BatchNorm3d) that the halo kernel runs (fp32, no grad)."""
+    if not (FILTER3D and x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
+            and not torch.is_autocast_enabled() and type(conv) is nn.Conv3d):
+        return False
+    kd, kh, kw = conv.kernel_size
+    if conv.stride != (1, 1, 1) or conv.dilation != (1, 1, 1) or conv.groups != 1 or kh != kw or kh not in (1, 3) \
+            or kd % 2 == 0 or conv.padding != (kd // 2, kh // 2, kw // 2):
+        return False
+    return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm3d and not bn.training
+                                                         and bn.track_running_stats)
+
+
+def _packed3d(conv, bn):
+    """Halo-kernel weights of conv with the eval BatchNorm folded in (fp64 fold), cached on conv."""
+    ts = [conv.weight] + ([conv.bias] if conv.bias is not None else [])
+    if isinstance(bn, nn.BatchNorm3d):
+        ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    key = tuple((t.data_ptr(), t._version) for t in ts)
+    hit = conv.__dict__.get("_fsmi_pack3d")
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            w = conv.weight.detach().double()
+            b = conv.bias.detach().double() if conv.bias is not None else torch.zeros(w.shape[0], dtype=w.dtype,
+                                                                                       device=w.device)
+            if isinstance(bn, nn.BatchNorm3d):
+                sc = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+                w = w * sc.view(-1, 1, 1, 1, 1)
+                b = (b - bn.running_mean.double()) * sc + bn.bias.double()
+            hit = (key, ops.PackedConv(w.float(), mode="halo"), b.float().contiguous())
+        conv.__dict__["_fsmi_pack3d"] = hit
+    return hit[1], hit[2]
+
+
+def conv3d_bn_act(x, conv, bn, act=None, res=None, res_pre=False):
+    """act(bn(conv(x)) [+ res]) on the halo kernel (see ``_fast3d`` for when it applies)."""
+    pk, b = _packed3d(conv, bn)
+    return ops.conv3d(x, pk, bias=b, act=act, res=res, res_pre=res_pre)
+
+
 def _norm(kind, ch, is_3d):
     if kind == "batch":
         return nn.BatchNorm3d(ch) if is_3d else nn.BatchNorm2d(ch)
@@ -65,6 +113,9 @@ class BasicConv(nn.Module):
             self.bn = _norm(norm, out_channels, is_3d)
 
     def forward(self, x):
+        bn = self.bn if self.use_bn else None
+        if _fast3d(x, self.conv, bn):        # stride-1 3D conv + folded BN + LeakyReLU, one kernel
+            return conv3d_bn_act(x, self.conv, bn, "leaky" if self.relu else None)
         x = self.bn(self.conv(x)) if self.use_bn else self.conv(x)
         return F.leaky_relu(x, 0.01) if self.relu else x
 
@@ -85,6 +136,11 @@ class Conv3dNormActReduced(nn.Module):
             norm(C_out), nn.ReLU())
 
     def forward(self, x):
+        c1, c2 = self.conv1, self.conv2
+        if _fast3d(x, c1[0], c1[1]) and _fast3d(x, c2[0], c2[1]) and isinstance(c1[2], nn.ReLU) \
+                and isinstance(c2[2], nn.ReLU):
+            y = conv3d_bn_act(x, c1[0], c1[1], "relu")
+            return conv3d_bn_act(y, c2[0], c2[1], "relu")
         return self.conv2(self.conv1(x))
 
 
@@ -112,6 +168,11 @@ class _ResBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        bn1 = self.bn1 if self.norm_layer is not None else None
+        bn2 = self.bn2 if self.norm_layer is not None else None
+        if self.downsample is None and _fast3d(x, self.conv1, bn1) and _fast3d(x, self.conv2, bn2):
+            y = conv3d_bn_act(x, self.conv1, bn1, "relu")
+            return conv3d_bn_act(y, self.conv2, bn2, "relu", res=x, res_pre=True)   # relu(bn2(conv2) + x)
         y = self.conv1(x)
         if self.norm_layer is not None:
             y = self.bn1(y)

@@ -198,6 +198,20 @@ int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* seg_ch, con
                              int out_ctot, int co0, int B, int Cout, int KS, int H, int W, int cfg, int nsplit,
                              float* ws, long long ws_floats, void* stream);
 
+/* ---- a3: 3D cost filtering (stride-1 Conv3d + folded BatchNorm) ----------
+ * replaces the stride-1 Conv3d+BN(+act) layers of core/submodule.py:51-195
+ * (BasicConv, Conv3dNormActReduced, ResnetBasicBlock3D) on MIOpen.  The same
+ * halo split-precision kernel: a KD x KS x KS conv (KS in {1,3}, KD odd, zero
+ * padding KD/2, KS/2) is the sum over kd of 2D convs on depth plane d+kd-KD/2.
+ * x (B,Cin,D,H,W), out / res (B,Cout,D,H,W); whi/wlo packed as for
+ * fsmi_conv2d_x3 with taps = (kd, kh, kw), kd major; bias = folded conv bias +
+ * BatchNorm shift.  out = act(conv + bias) + res, or with res_pre
+ * act(conv + bias + res); act 0 none, 1 ReLU, 6 LeakyReLU(0.01).
+ * cfg as fsmi_conv2d_halo_x3 plus 6: 32 couts x 8x32 px, 7: 32 x 4x32. */
+int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wlo, int wexp, const float* bias,
+                        const float* res, float* out, int B, int Cout, int D, int H, int W, int KD, int KS,
+                        int act, int res_pre, int cfg, int nsplit, float* ws, long long ws_floats, void* stream);
+
 /* ---- refinement-loop auxiliaries ---------------------------------------
  * fsmi_dwconv2d: depthwise KSxKS conv (KS in {3,5,7}, stride 1, zero pad KS/2)
  *   x, out (B,C,H,W); w (C,1,KS,KS); bias (C) or NULL.  Replaces the EdgeNeXt

@@ -174,6 +174,53 @@ def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
 
 
+@pytest.mark.parametrize("cfg", [-1, 5, 6, 7])
+@pytest.mark.parametrize("kern,cin,cout,D,act,res", [((3, 3, 3), 28, 28, 7, "leaky", None),
+                                                     ((1, 3, 3), 28, 28, 5, "relu", None),
+                                                     ((17, 1, 1), 28, 28, 20, "relu", None),
+                                                     ((1, 1, 1), 56, 28, 6, None, "post"),
+                                                     ((3, 3, 3), 28, 28, 4, "relu", "pre"),
+                                                     ((3, 3, 3), 40, 37, 3, None, None)])
+def test_conv3d_halo_vs_torch(ops_mod, kern, cin, cout, D, act, res, cfg):
+    """Stride-1 Conv3d on the halo kernel (sum over kd of 2D planes): 3^3, axial (1,3,3) and
+    (17,1,1), 1^3 with a residual, the ResNet tail act(conv + res), ragged channels / tiles,
+    auto split-K; vs fp64 torch.  2e-5 abs + 1e-5 rel as the 2D halo conv."""
+    import torch.nn.functional as F
+    B, H, W = 1, 9, 37
+    x = synth.normal(501, (B, cin, D, H, W))
+    w = synth.normal(502, (cout, cin) + kern, 0.15)
+    bias = synth.normal(503, (cout,), 0.1)
+    r = synth.normal(504, (B, cout, D, H, W)) if res else None
+    pk = ops_mod.PackedConv(g(w), mode="halo")
+    out = ops_mod.conv3d(g(x), pk, bias=g(bias), act=act, res=g(r) if res else None, res_pre=res == "pre", cfg=cfg)
+    y = F.conv3d(t(x).double(), t(w).double(), t(bias).double(), padding=tuple(k // 2 for k in kern))
+    if res == "pre":
+        y = y + t(r).double()
+    y = {"relu": F.relu, "leaky": lambda v: F.leaky_relu(v, 0.01), None: lambda v: v}[act](y)
+    if res == "post":
+        y = y + t(r).double()
+    close(out, y, atol=2e-5, rtol=1e-5)
+
+
+def test_filter3d_blocks_vs_torch(ops_mod):
+    """BasicConv(3D) / ResnetBasicBlock3D / Conv3dNormActReduced fast paths (BatchNorm folded into
+    the packed weights) vs the same modules in fp64 on the CPU (torch path)."""
+    import copy
+    from foundationstereo_amd.submodule import BasicConv, Conv3dNormActReduced, ResnetBasicBlock3D
+    mods = [BasicConv(28, 28, is_3d=True, kernel_size=3, padding=1, stride=1),
+            ResnetBasicBlock3D(28, 28, kernel_size=3, stride=1, padding=1),
+            Conv3dNormActReduced(28, 28, kernel_size=3, kernel_disp=17)]
+    x = synth.normal(511, (1, 28, 18, 10, 33))
+    for i, m in enumerate(mods):
+        synth.init_module_(m, seed=520 + i)
+        m.eval()
+        ref = copy.deepcopy(m).double()
+        with torch.no_grad():
+            out = m.to(DEV)(g(x))
+            want = ref(t(x).double())
+        close(out, want, atol=3e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("KS,shape", [(7, (2, 5, 19, 70)), (7, (1, 3, 120, 160)), (3, (1, 4, 17, 9)),
                                       (5, (1, 2, 33, 65))])
 def test_dwconv2d_vs_torch(ops_mod, KS, shape):
