@@ -68,10 +68,11 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB):
-        raise FsmiError(f"libfsmi.so not found at {LIB}: the HIP hot path is not built "
+    path = os.environ.get("FSMI_LIB", LIB)   # A/B builds of the same ABI (tools/); default in-tree
+    if not os.path.exists(path):
+        raise FsmiError(f"libfsmi.so not found at {path}: the HIP hot path is not built "
                         "(run `python -m foundationstereo_amd.build`)")
-    lib = ctypes.CDLL(LIB)
+    lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes

@@ -443,6 +443,10 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
       } else {
         load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
       }
+      // issue the next tap's loads before this tap's MFMAs: unfenced, the scheduler sinks them
+      // below the last MFMA and reuses the current buffer's registers -- a single buffer whose
+      // L2 round trip every tap then waits on
+      __builtin_amdgcn_sched_barrier(0);
       const int dh = tap / KS, dw = tap % KS;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {

@@ -12,6 +12,9 @@ from __future__ import annotations
 
 from typing import List, Sequence
 
+import json
+import os
+
 import torch
 
 from . import _lib
@@ -354,7 +357,8 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
     if _CONV_FLOPS["on"]:
         _CONV_FLOPS["flops"] += 2 * Cin * pk.cout * pk.kd * pk.k * pk.k * B * D * H * W
     stream = _stream(x)
-    ws = _split_workspace(x.device, stream, 4 * B * pk.cout * D * H * W)
+    ws = _split_workspace(x.device, stream, 8 * B * pk.cout * D * H * W)
+    cfg, nsplit = _tuned(pk.k, pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
     _lib.check(_lib.load().fsmi_conv3d_halo_x3(
         _p(x), Cin, _p(pk.whi), _p(pk.wlo), pk.wexp, _p(bias) if bias is not None else None,
         _p(res) if res is not None else None, _p(out), B, pk.cout, D, H, W, pk.kd, pk.k, _ACT3D[act],
@@ -392,12 +396,42 @@ def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Te
         _CONV_FLOPS["flops"] += 2 * cin * pk.cout * pk.k * pk.k * B * H * W
     stream = _stream(t0)
     ws = _split_workspace(t0.device, stream, 8 * B * pk.cout * H * W)
+    cfg, nsplit = _tuned(pk.k, 1, cin, pk.cout, B, 1, H, W, cfg, nsplit)
     _lib.check(_lib.load().fsmi_conv2d_halo_x3_gate(
         pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, _p(bias), m, _p(h), _p(z),
         _p(att) if att is not None else None, _p(rh) if rh is not None else None, Hd,
         _p(out) if out is not None else None, out.shape[1] if out is not None else 0, 0, B, pk.cout, pk.k, H, W,
         cfg, nsplit, _p(ws), ws.numel(), stream), "conv2d_gate")
     del keep
+
+
+# ---- measured tile / split-K choices per conv shape (tools/tune_conv.py -> tuning/fsmi_conv.json):
+# consulted when a caller leaves cfg / nsplit on auto; shapes not in the table use the C-side policy
+_TUNE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "fsmi_conv.json")
+_TUNE = None
+_RECORD = None          # set of shape keys while tools/tune_conv.py records a forward
+
+
+def _tune_key(ks, kd, cin, cout, B, D, H, W) -> str:
+    return f"k{ks}_d{kd}_ci{cin}_co{cout}_b{B}_D{D}_h{H}_w{W}"
+
+
+def _tuned(ks, kd, cin, cout, B, D, H, W, cfg, nsplit):
+    global _TUNE
+    key = _tune_key(ks, kd, cin, cout, B, D, H, W)
+    if _RECORD is not None:
+        _RECORD.add(key)
+    if cfg >= 0 and nsplit >= 0 or os.environ.get("FSMI_TUNE_DB", "1") == "0":
+        return cfg, nsplit
+    if _TUNE is None:
+        _TUNE = {}
+        if os.path.exists(_TUNE_PATH):
+            with open(_TUNE_PATH) as f:
+                _TUNE = json.load(f).get("entries", {})
+    e = _TUNE.get(key)
+    if e is None:
+        return cfg, nsplit
+    return (e["cfg"] if cfg < 0 else cfg), (e["nsplit"] if nsplit < 0 else nsplit)
 
 
 _SPLIT_WS = {}
@@ -453,7 +487,8 @@ def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=N
     else:
         # auto split-K is capped at 8; the workspace covers that for this output
         ws = _split_workspace(t0.device, common[-1], 8 * B * pk.cout * H * W)
-        hc = common[:9] + (pk.k,) + common[11:-1] + (nsplit, _p(ws), ws.numel(), common[-1])
+        tcfg, nsplit = _tuned(pk.k, 1, cin, pk.cout, B, 1, H, W, cfg, nsplit)
+        hc = common[:9] + (pk.k,) + common[11:-2] + (tcfg, nsplit, _p(ws), ws.numel(), common[-1])
         _lib.check(lib.fsmi_conv2d_halo_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, *hc),
                    "conv2d_halo_x3")
     del keep

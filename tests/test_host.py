@@ -100,3 +100,19 @@ def test_synth_is_deterministic():
     b = synth.normal(synth.name_seed("x"), (4, 5))
     assert np.array_equal(a, b)
     assert abs(float(synth.normal(7, (100000,)).std()) - 1.0) < 0.02
+
+
+def test_conv_tuning_db_wellformed():
+    """tuning/fsmi_conv.json (tools/tune_conv.py) parses, and every entry names a valid tile
+    config / split factor for a well-formed shape key."""
+    import json
+    import re
+    from foundationstereo_amd import ops
+    with open(ops._TUNE_PATH) as f:
+        db = json.load(f)
+    assert db["entries"], "empty tuning table"
+    for key, e in db["entries"].items():
+        ks, kd, cin, cout, B, D, H, W = (int(v) for v in re.findall(r"\d+", key))
+        assert key == ops._tune_key(ks, kd, cin, cout, B, D, H, W)
+        assert ks in (1, 3) and kd % 2 == 1 and min(cin, cout, B, D, H, W) > 0
+        assert 0 <= e["cfg"] <= 7 and 1 <= e["nsplit"] <= 8

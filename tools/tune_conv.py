@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Measure the best tile config / split-K factor of every halo-conv shape one forward uses and
+write them to tuning/fsmi_conv.json (read by ops.conv2d / conv2d_gate / conv3d when the caller
+leaves cfg / nsplit on auto).  Run on the GPU box:
+
+    python tools/tune_conv.py [--config cfg2] [--reps 5]
+"""
+import argparse
+import json
+import os
+import re
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from foundationstereo_amd import ops, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="cfg2")
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+
+sys.path.insert(0, REPO)
+import bench  # noqa: E402  (workload table)
+
+H, W, md, iters, vit, per_gpu = bench.CONFIGS[a.config]
+args = synth.make_args(max_disp=md, corr_levels=4, vit_size=vit)
+model = bench.make_model(args, dev, 0)
+feats = [synth.backbone_features(1, H, W, vit, seed=0x5EED + i, shift_px=8) for i in range(per_gpu)]
+fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(dev) for j in range(4)]
+fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(dev) for j in range(4)]
+vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(dev)
+model.feature.set_features(fl, fr, vf)
+left, right = synth.stereo_images(per_gpu, H, W)
+
+# 1. record the shapes of one forward (tuning table disabled so every call is on auto)
+os.environ["FSMI_TUNE_DB"] = "0"
+ops._RECORD = set()
+with torch.no_grad():
+    model(torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev), iters=2, test_mode=True)
+torch.cuda.synchronize()
+keys = sorted(ops._RECORD)
+ops._RECORD = None
+print(f"[tune] {len(keys)} conv shapes", file=sys.stderr)
+
+
+def timeit(fn):
+    fn()
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / a.reps
+
+
+entries = {}
+t_start = time.time()
+with torch.no_grad():
+    for key in keys:
+        ks, kd, cin, cout, B, D, Hh, Ww = (int(v) for v in re.findall(r"\d+", key))
+        if kd == 1 and D == 1:
+            x = torch.randn(B, cin, Hh, Ww, device=dev)
+            w = torch.randn(cout, cin, ks, ks, device=dev) * 0.05
+        else:
+            x = torch.randn(B, cin, D, Hh, Ww, device=dev)
+            w = torch.randn(cout, cin, kd, ks, ks, device=dev) * 0.05
+        b = torch.randn(cout, device=dev)
+        pk = ops.PackedConv(w, mode="halo")
+
+        def run(cfg, ns):
+            if x.dim() == 4:
+                return ops.conv2d([x], pk, bias=b, act="relu", cfg=cfg, nsplit=ns)
+            return ops.conv3d(x, pk, bias=b, act="relu", cfg=cfg, nsplit=ns)
+
+        nck = kd * ((cin + 31) // 32)
+        cfgs = [2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
+        splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck)]
+        auto = timeit(lambda: run(-1, -1))
+        best = (auto, -1, -1)
+        for c in cfgs:
+            for s in splits:
+                t = timeit(lambda: run(c, s))
+                if t < best[0]:
+                    best = (t, c, s)
+        if best[1] >= 0:
+            entries[key] = {"cfg": best[1], "nsplit": best[2], "us": round(best[0], 1), "auto_us": round(auto, 1)}
+        print(json.dumps({"key": key, "auto_us": round(auto, 1), "best_us": round(best[0], 1), "cfg": best[1],
+                          "nsplit": best[2]}), flush=True)
+
+os.makedirs(os.path.dirname(a.out), exist_ok=True)
+with open(a.out, "w") as f:
+    json.dump({"device": torch.cuda.get_device_name(0), "config": a.config, "source": "tools/tune_conv.py",
+               "entries": entries}, f, indent=1, sort_keys=True)
+print(f"[tune] wrote {len(entries)} entries to {a.out} in {time.time() - t_start:.0f}s", file=sys.stderr)
