@@ -705,7 +705,7 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
                                    int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
                                    long long ws_floats, void* stream) {
   FSMI_CHECK_ARG(out, "fsmi_conv2d_halo_x3: null output");
-  FSMI_CHECK_ARG(act >= 0 && act <= 2, "fsmi_conv2d_halo_x3: act %d", act);
+  FSMI_CHECK_ARG((act >= 0 && act <= 2) || act == 6, "fsmi_conv2d_halo_x3: act %d (0, 1, 2, 6)", act);
   HaloArgs a{};
   a.act = act;
   a.alpha = alpha;

@@ -14,7 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import synth
-from .submodule import BasicConv
+from .submodule import BasicConv, _fast2d, conv2d_bn_act
 
 __all__ = ["ResidualBlock", "ContextNetDino", "DepthAnythingFeature", "SyntheticFeature"]
 
@@ -55,11 +55,30 @@ class ResidualBlock(nn.Module):
                                         self.norm3) if proj else None
 
     def forward(self, x):
+        n1 = self.norm1 if isinstance(self.norm1, nn.BatchNorm2d) else None
+        n2 = self.norm2 if isinstance(self.norm2, nn.BatchNorm2d) else None
+        if n1 is not None and n2 is not None and _fast2d(x, self.conv2, n2):
+            # stride-1 convs on the halo kernel with the eval BN folded in; the strided first conv
+            # of a downsampling block and its 1x1 projection stay on MIOpen
+            y = conv2d_bn_act([x], self.conv1, n1, "relu") if _fast2d(x, self.conv1, n1) \
+                else F.relu(n1(self.conv1(x)))
+            y = conv2d_bn_act([y], self.conv2, n2, "relu")
+            if self.downsample is not None:
+                x = self.downsample(x)
+            return torch.relu_(y.add_(x))
         y = F.relu(self.norm1(self.conv1(x)))
         y = F.relu(self.norm2(self.conv2(y)))
         if self.downsample is not None:
             x = self.downsample(x)
         return F.relu(x + y)
+
+
+def _head(f, x):
+    """Output head: [ResidualBlock,] Conv2d(3x3, bias); the conv on the halo kernel when it can."""
+    if isinstance(f, nn.Conv2d):
+        return conv2d_bn_act([x], f, None) if _fast2d(x, f, None) else f(x)
+    x = f[0](x)
+    return conv2d_bn_act([x], f[1], None) if _fast2d(x, f[1], None) else f[1](x)
 
 
 class ContextNetDino(nn.Module):
@@ -101,12 +120,15 @@ class ContextNetDino(nn.Module):
     def forward(self, x_in, vit_feat, dual_inp=False, num_layers=3):
         x = self.relu1(self.norm1(self.conv1(x_in)))
         x = self.layer3(self.layer2(self.layer1(x)))
-        x = self.conv2(torch.cat([x, vit_feat], dim=1))
-        o4 = [f(x) for f in self.outputs04]
+        if _fast2d(x, self.conv2.conv, self.conv2.bn) and vit_feat.is_contiguous() and x.shape[1] % 8 == 0:
+            x = conv2d_bn_act([x, vit_feat], self.conv2.conv, self.conv2.bn, "leaky")   # cat as segments
+        else:
+            x = self.conv2(torch.cat([x, vit_feat], dim=1))
+        o4 = [_head(f, x) for f in self.outputs04]
         y = self.layer4(x)
-        o8 = [f(y) for f in self.outputs08]
+        o8 = [_head(f, y) for f in self.outputs08]
         z = self.layer5(y)
-        o16 = [f(z) for f in self.outputs16]
+        o16 = [_head(f, z) for f in self.outputs16]
         return o4, o8, o16
 
 

@@ -273,7 +273,7 @@ def pack_conv_weight(*weights: Tensor) -> Tensor:
     return pk
 
 
-ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "leaky": 6}   # leaky: halo kernel only
 
 
 class PackedConv:

@@ -5,9 +5,9 @@ so ``core.foundation_stereo`` can star-import this module instead
 (SURVEY §8b).  The cost-volume functions, ``disparity_regression`` and
 ``context_upsample`` run the hand-written gfx950 kernels of ``libfsmi.so``.
 Stride-1 3D conv blocks (``BasicConv``, ``Conv3dNormActReduced``,
-``ResnetBasicBlock3D``) run the halo split-precision conv kernel with the eval
-BatchNorm folded into the packed weights (``conv3d_bn_act``); strided / transposed
-3D convs and the 2D feature convs stay on MIOpen through ``torch.nn``.
+``ResnetBasicBlock3D``) and stride-1 2D ``BasicConv``s run the halo split-precision
+conv kernel with the eval BatchNorm folded into the packed weights (``conv3d_bn_act``,
+``conv2d_bn_act``); strided / transposed convs stay on MIOpen through ``torch.nn``.
 
 The disparity transformer's attention uses PyTorch SDPA in place of the
 reference's third-party ``flash_attn_func`` (core/submodule.py:224): same
@@ -64,30 +64,51 @@ def _fast3d(x, conv, bn) -> bool:
                                                          and bn.track_running_stats)
 
 
-def _packed3d(conv, bn):
-    """Halo-kernel weights of conv with the eval BatchNorm folded in (fp64 fold), cached on conv."""
+def _fast2d(x, conv, bn) -> bool:
+    """Stride-1 'same' Conv2d (1x1 / 3x3, + eval BatchNorm2d) that the halo kernel runs."""
+    if not (FILTER3D and x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
+            and not torch.is_autocast_enabled() and type(conv) is nn.Conv2d):
+        return False
+    kh, kw = conv.kernel_size
+    if conv.stride != (1, 1) or conv.dilation != (1, 1) or conv.groups != 1 or kh != kw or kh not in (1, 3) \
+            or conv.padding != (kh // 2, kw // 2):
+        return False
+    return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm2d and not bn.training
+                                                         and bn.track_running_stats)
+
+
+def _packed_bn(conv, bn):
+    """Halo-kernel weights of a Conv2d/Conv3d with its eval BatchNorm folded in (fp64 fold),
+    cached on the conv module, rebuilt when any parameter or running statistic changes."""
     ts = [conv.weight] + ([conv.bias] if conv.bias is not None else [])
-    if isinstance(bn, nn.BatchNorm3d):
+    is_bn = isinstance(bn, (nn.BatchNorm2d, nn.BatchNorm3d))
+    if is_bn:
         ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
     key = tuple((t.data_ptr(), t._version) for t in ts)
-    hit = conv.__dict__.get("_fsmi_pack3d")
+    hit = conv.__dict__.get("_fsmi_pack_bn")
     if hit is None or hit[0] != key:
         with torch.no_grad():
             w = conv.weight.detach().double()
             b = conv.bias.detach().double() if conv.bias is not None else torch.zeros(w.shape[0], dtype=w.dtype,
                                                                                        device=w.device)
-            if isinstance(bn, nn.BatchNorm3d):
+            if is_bn:
                 sc = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
-                w = w * sc.view(-1, 1, 1, 1, 1)
+                w = w * sc.view((-1,) + (1,) * (w.dim() - 1))
                 b = (b - bn.running_mean.double()) * sc + bn.bias.double()
             hit = (key, ops.PackedConv(w.float(), mode="halo"), b.float().contiguous())
-        conv.__dict__["_fsmi_pack3d"] = hit
+        conv.__dict__["_fsmi_pack_bn"] = hit
     return hit[1], hit[2]
+
+
+def conv2d_bn_act(segs, conv, bn, act=None, **kw):
+    """act(bn(conv(cat(segs)))) on the 2D halo kernel (see ``_fast2d``); ``segs`` as ops.conv2d."""
+    pk, b = _packed_bn(conv, bn)
+    return ops.conv2d(segs, pk, bias=b, act=act, **kw)
 
 
 def conv3d_bn_act(x, conv, bn, act=None, res=None, res_pre=False):
     """act(bn(conv(x)) [+ res]) on the halo kernel (see ``_fast3d`` for when it applies)."""
-    pk, b = _packed3d(conv, bn)
+    pk, b = _packed_bn(conv, bn)
     return ops.conv3d(x, pk, bias=b, act=act, res=res, res_pre=res_pre)
 
 
@@ -116,6 +137,8 @@ class BasicConv(nn.Module):
         bn = self.bn if self.use_bn else None
         if _fast3d(x, self.conv, bn):        # stride-1 3D conv + folded BN + LeakyReLU, one kernel
             return conv3d_bn_act(x, self.conv, bn, "leaky" if self.relu else None)
+        if _fast2d(x, self.conv, bn):
+            return conv2d_bn_act([x], self.conv, bn, "leaky" if self.relu else None)
         x = self.bn(self.conv(x)) if self.use_bn else self.conv(x)
         return F.leaky_relu(x, 0.01) if self.relu else x
 

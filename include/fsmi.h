@@ -146,7 +146,8 @@ int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float*
  *   seg_ctot[i] channels per image (batch stride seg_ctot[i]*H*W).
  * wpk: weights packed [KH*KW*Cin][roundup(Cout,4)] (k = (kh*KW+kw)*Cin + ci), zero padded.
  * out[b, co0+co] (tensor with out_ctot channels) =
- *   res[b,co] + gamma[co] * alpha * act(conv + bias[co]);  act 0 none, 1 ReLU, 2 GELU(erf);
+ *   res[b,co] + gamma[co] * alpha * act(conv + bias[co]);  act 0 none, 1 ReLU, 2 GELU(erf)
+ *   (fsmi_conv2d_halo_x3 also 6: LeakyReLU 0.01);
  *   bias/gamma/res may be NULL (res has res_ctot channels per image).
  * KHxKW in {1x1, 3x3, 7x7}, stride 1, zero padding K/2.  cfg: tile config or -1 (auto). */
 int fsmi_conv2d(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,

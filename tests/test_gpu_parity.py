@@ -221,6 +221,27 @@ def test_filter3d_blocks_vs_torch(ops_mod):
         close(out, want, atol=3e-5, rtol=1e-5)
 
 
+def test_context_blocks_vs_torch(ops_mod):
+    """Context-net fast paths (BN folded into halo convs): ResidualBlock with and without a
+    strided projection, the 2D BasicConv with LeakyReLU, and the ContextNetDino output heads,
+    vs the same modules in fp64 on the CPU."""
+    import copy
+    from foundationstereo_amd.extractor import ResidualBlock
+    from foundationstereo_amd.submodule import BasicConv
+    cases = [(ResidualBlock(64, 64, "batch", stride=1), (1, 64, 24, 40)),
+             (ResidualBlock(64, 96, "batch", stride=2), (1, 64, 24, 40)),
+             (BasicConv(136, 128, kernel_size=3, padding=1), (1, 136, 17, 33))]
+    for i, (m, shape) in enumerate(cases):
+        synth.init_module_(m, seed=530 + i)
+        m.eval()
+        ref = copy.deepcopy(m).double()
+        x = synth.normal(540 + i, shape)
+        with torch.no_grad():
+            out = m.to(DEV)(g(x))
+            want = ref(t(x).double())
+        close(out, want, atol=3e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("KS,shape", [(7, (2, 5, 19, 70)), (7, (1, 3, 120, 160)), (3, (1, 4, 17, 9)),
                                       (5, (1, 2, 33, 65))])
 def test_dwconv2d_vs_torch(ops_mod, KS, shape):
