@@ -56,10 +56,11 @@ def _packed(*mods):
 _SIDE = {}
 
 
-def _side_stream(device):
-    s = _SIDE.get(device)
+def _side_stream(device, idx=0):
+    """Side stream ``idx`` of ``device`` (0: motion path, 1: GRU small branch / mask head)."""
+    s = _SIDE.get((device, idx))
     if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device)
+        s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device)
     return s
 
 
@@ -224,11 +225,29 @@ class SelectiveConvGRU(nn.Module):
                 return ops.gru_blend(zr_s, zr_l, q_s, q_l, h, att.float())
             att = att.float().contiguous()
             out = torch.empty_like(h)
-            for gru, mode in ((self.small_gru, "blend_small"), (self.large_gru, "blend_large")):
+
+            def branch(gru, mode):
                 z, rh = torch.empty_like(h), torch.empty_like(h)
                 pk, b = _packed(gru.convz, gru.convr)
                 ops.conv2d_gate([hx], pk, b, "zr", h=h, z=z, rh=rh)
                 pk, b = _packed(gru.convq)
+                return pk, b, z, rh
+
+            if OVERLAP:
+                # small (1x1) branch on a side stream beside the large branch's zr conv; the
+                # large blend adds into ``out`` after the small blend has written it
+                main = torch.cuda.current_stream(h.device)
+                side = _side_stream(h.device, 1)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    pk, b, z, rh = branch(self.small_gru, "blend_small")
+                    ops.conv2d_gate([rh, xc], pk, b, "blend_small", h=h, z=z, att=att, out=out)
+                pk, b, z, rh = branch(self.large_gru, "blend_large")
+                main.wait_stream(side)
+                ops.conv2d_gate([rh, xc], pk, b, "blend_large", h=h, z=z, att=att, out=out)
+                return out
+            for gru, mode in ((self.small_gru, "blend_small"), (self.large_gru, "blend_large")):
+                pk, b, z, rh = branch(gru, mode)
                 ops.conv2d_gate([rh, xc], pk, b, mode, h=h, z=z, att=att, out=out)
             return out
         x = torch.cat(x, dim=1) if len(x) > 1 else x[0]
@@ -305,8 +324,13 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         main.wait_stream(side)
         if n > 1:
             net[0] = self.gru04(att[0], net[0], inp[0], enc, interp(net[1], net[0]))
+        # mask head beside the disparity head (both read net[0] only)
+        side1 = _side_stream(disp.device, 1)
+        side1.wait_stream(main)
+        with torch.cuda.stream(side1):
+            mask = _conv(self.mask[2], [_conv(self.mask[0], [net[0]], "relu")], "relu", alpha=0.25)
         delta_disp = self.disp_head(net[0])
-        mask = _conv(self.mask[2], [_conv(self.mask[0], [net[0]], "relu")], "relu", alpha=0.25)
+        main.wait_stream(side1)
         return net, mask, delta_disp
 
     def _forward_fast(self, net, inp, corr, disp, att):
