@@ -180,12 +180,16 @@ def main():
         elapsed = float(t.item())
     if a.graph:
         # graph replays carry no per-kernel events (HIP rejects external event nodes during
-        # capture): time the kernels over one eager pass of the identical step instead
+        # capture): time the kernels over one eager pass of the identical step instead, on one
+        # stream -- with the side-stream overlap on, a kernel's event span would include the
+        # time it shares the chip with another stream's kernels
+        overlap, fupdate.OVERLAP = fupdate.OVERLAP, False
         ops.timer_enable(True)
         ops.timer_reset()
         runner._graph, saved = None, runner._graph
         step()
         runner._graph = saved
+        fupdate.OVERLAP = overlap
     lk_ms, lk_n = ops.timer_query("lookup")
     cb_ms, cb_n = ops.timer_query("comb")
     cv_ms, cv_n = ops.timer_query("conv2d")
@@ -228,13 +232,13 @@ def main():
                    "corr_levels": L, "conv_engine": a.conv_engine, "hip_graph": bool(a.graph),
                    "parallelism": f"dp{world}"},
         "roofline": {"kernel": "geo_lookup", "bound": "hbm",
-                     "timed_over": "eager step after the timed region" if a.graph else "timed region", "achieved": lk_bytes / lk_avg / 1e9,
+                     "timed_over": "single-stream eager step after the timed region" if a.graph else "timed region", "achieved": lk_bytes / lk_avg / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
                      "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,
                      "launches": lk_n},
         # the refinement-loop convs (halo-tiled 3 x fp16 MFMA, split-K reduce included) hold most of
         # the step time; algorithmic = fp32 conv FLOPs, peak = dense fp16 MFMA / 3 products per MAC
-        "roofline_conv": {"kernel": "conv2d_halo_x3 (all loop convs)", "bound": "mfma",
+        "roofline_conv": {"kernel": "conv*_halo_x3 (all halo convs: loop, 3D filter, context net)", "bound": "mfma",
                           "achieved": cv_flops / (cv_ms / 1e3) / 1e12 if cv_n else None,
                           "peak": MFMA_F16_PEAK / 3 / 1e12, "unit": "TFLOP/s",
                           "frac": cv_flops / (cv_ms / 1e3) / (MFMA_F16_PEAK / 3) if cv_n else None,

@@ -211,10 +211,20 @@ __device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
   t.split = cs - ctile * a.nsplit;
   t.m0 = ctile * BM;
   const int per_plane = a.nrt * a.nct;
-  const int bd = ptile / per_plane;                // (image, depth plane)
-  t.b = D3 ? bd / a.D : bd;
-  t.d0 = D3 ? bd - t.b * a.D : 0;
-  const int prem = ptile - bd * per_plane;
+  int prem;
+  if constexpr (D3) {
+    // depth fastest: blocks of consecutive output depths at one (row, col) tile run together on
+    // one XCD, so the KD input planes each of them reads are shared in that XCD's L2 (depth-
+    // slowest order re-fetched them from HBM: 10x the input for a (17,1,1) conv)
+    t.d0 = ptile % a.D;
+    const int rest = ptile / a.D;
+    t.b = rest / per_plane;
+    prem = rest - t.b * per_plane;
+  } else {
+    t.b = ptile / per_plane;
+    t.d0 = 0;
+    prem = ptile - t.b * per_plane;
+  }
   t.r0 = (prem / a.nct) * TR;
   t.c0 = (prem % a.nct) * 32;
   return t;
