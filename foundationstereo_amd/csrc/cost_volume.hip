@@ -9,6 +9,8 @@
 // in LDS once and normalised there, every output lane writes consecutive w so
 // stores are coalesced 256 B per wave-instruction.  Blocks of the same row
 // are placed on one XCD (xcd_remap) so re-staging a row hits that XCD's L2.
+#include <cstdlib>
+
 #include "fsmi_common.h"
 
 namespace fsmi {
@@ -215,110 +217,285 @@ __global__ __launch_bounds__(kThreads) void stem_stream_kernel(const float* __re
   }
 }
 
-// a1 + a2 + corr_stem[0] (1x1x1 conv 32 -> Cs):
-// out[b,o,d,h,w] = A[o,w] + [w>=d] Bm[o,w-d] + sum_g Wg[o,g] gwc_g(d,w)
+// a1 + a2 + corr_stem[0] (1x1x1 conv 32 -> Cs) in ONE streaming pass, no gwc scratch:
+//   out[b,o,d,h,w] = A[b,o,h,w] + Bm[b,o,h,w-d] (w >= d) + sum_g Wg[o,g] gwc_g(d,w)
+// (A / Bm = the proj_cmb halves of the concat volume folded through the stem weight, bias in A).
 //
-// Block = one (b,h) row x DC disparities.  Phase 1 walks the G groups: stage
-// the normalised group rows of fl/fr in LDS, each thread computes the group
-// correlation of VEC consecutive w for one d (one ds_read_b128 of L per
-// channel) into an LDS gwc tile [G][DC][W].  Phase 2 re-uses the staging
-// space for the A/Bm rows and emits all Cs output channels of VEC consecutive
-// w per item as 16-B stores (one 1-KiB coalesced store per wave-instruction).
-template <int G, int VEC>
-__global__ __launch_bounds__(kThreads) void comb_stem_kernel(const float* __restrict__ fl,
-                                                             const float* __restrict__ fr,
-                                                             const float* __restrict__ A,
-                                                             const float* __restrict__ Bm,
-                                                             const float* __restrict__ Wg,
-                                                             float* __restrict__ out, int C, int Cs, int D,
-                                                             int H, int W, int DC, int nDC) {
+// Block = (b, h, WT = 4*WQ column tile, DCH = 4*DQN disparity chunk); thread = 4 d x 4 w, so a
+// wave-instruction store covers 4 rows of 256 contiguous bytes.  Measured per-block timeline
+// (tools/build_phases.py) drove the structure: every block runs at once (~1 wave per SIMD at
+// cfg2), so each dependent global round trip costs ~3 us and the volume stores, all issued in one
+// phase, run at the chip's write rate (~7 TB/s); the kernel is therefore
+//   1. ONE staging round trip: the fl rows (WT columns), the fr rows (the WT + DCH columns the
+//      chunk's shifts reach), the A / Bm rows and the stem columns go global -> LDS by LDS-DMA
+//      (global_load_lds_dwordx4, no VGPR staging), one s_waitcnt + barrier per phase (one phase
+//      when the image fits ~80 KB -- ViT-S -- else groups in NPH phases);
+//      columns outside [0, W) are written as zeros, so w < d needs no masking anywhere;
+//   2. per channel one float4 of L and two aligned float4 of R (the 7-wide shift window) feed
+//      16 packed-FMA dot products; one thread per staged column sums its squared norm;
+//   3. F.normalize (eps 1e-12, core/submodule.py:395) applied after the dots:
+//      gwc = (L . R) * inv|L| * inv|R|, then the Cs-channel stem epilogue and 16-B stores.
+// Blocks of one row are neighbours in the XCD remap (shared L2 for the overlapping R rows).
+constexpr int kBuildG = 8;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// 4 columns [col, col+4) of a row; zeros outside [0, W)
+__device__ __forceinline__ float4 build_quad1(const float* p, int col, int W) {
+  float4 v;
+  v.x = (col + 0 >= 0 && col + 0 < W) ? p[0] : 0.f;
+  v.y = (col + 1 >= 0 && col + 1 < W) ? p[1] : 0.f;
+  v.z = (col + 2 >= 0 && col + 2 < W) ? p[2] : 0.f;
+  v.w = (col + 3 >= 0 && col + 3 < W) ? p[3] : 0.f;
+  return v;
+}
+
+// rows x cols (multiple of 4) columns from col0 of channel-strided rows -> lds[rows][cols], element
+// e = (row, column quad) at lds + 4e.  VEC 4 (W % 4 == 0, quads wholly in or out of [0, W)):
+// LDS-DMA, one 1-KiB wave-instruction per 64 consecutive elements (destination = wave-uniform
+// base + 16 * lane), zero quads by ds_write; VEC 1: register path with per-element bounds.
+template <int VEC>
+__device__ __forceinline__ void build_stage_rows(const float* __restrict__ f, size_t plane, int rows, int cols,
+                                                 int col0, int W, float* lds, int tid, int nthr) {
+  const int nq = cols / 4, n = rows * nq;
+  const int sc = nthr / nq, sq = nthr - sc * nq;
+  int c = tid / nq, q = tid - c * nq;
+  const int wbase = tid & ~(kWave - 1);
+  for (int e0 = 0; e0 < n; e0 += nthr) {
+    const int e = e0 + tid;
+    if (e < n) {
+      const int col = col0 + 4 * q;
+      const float* src = f + static_cast<size_t>(c) * plane + col;
+      if constexpr (VEC == 4) {
+        if (col >= 0 && col < W)
+          __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(lds + 4 * (e0 + wbase)), 16, 0, 0);
+        else
+          *reinterpret_cast<float4*>(lds + 4 * e) = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        *reinterpret_cast<float4*>(lds + 4 * e) = build_quad1(src, col, W);
+      }
+    }
+    q += sq;
+    c += sc;
+    if (q >= nq) {
+      q -= nq;
+      ++c;
+    }
+  }
+}
+
+// LDS image (floats): [A: Cs x WT][Bm: Cs x RS][Wg: Cs x G][invn: G x (WT+RS)][groups: GP x Cg x (WT+RS)]
+__host__ __device__ inline int build_lds_floats(int Cg, int Cs, int WT, int RS, int GP) {
+  return Cs * (WT + RS) + Cs * kBuildG + kBuildG * (WT + RS) + GP * Cg * (WT + RS);
+}
+
+template <int VEC, int GP>
+__global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __restrict__ fl,
+                                                              const float* __restrict__ fr,
+                                                              const float* __restrict__ A,
+                                                              const float* __restrict__ Bm,
+                                                              const float* __restrict__ Wg,
+                                                              float* __restrict__ out, int C, int Cs, int D,
+                                                              int H, int W, int WQ, int DQN, int nwt, int ndc, int dbg) {
+  constexpr int G = kBuildG, NPH = G / GP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Cg = C / G;
+  const int WT = 4 * WQ, DCH = 4 * DQN, RS = WT + DCH, NC = WT + RS;
   const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
-  const int row = item / nDC, dc = item - row * nDC;
+  const int dc = item % ndc;
+  const int rest = item / ndc;
+  const int wt = rest % nwt;
+  const int row = rest / nwt;
   const int b = row / H, h = row - b * H;
-  const int d0 = dc * DC, dn = min(DC, D - d0);
+  const int w0 = wt * WT, d0 = dc * DCH;
+  const int rs0 = w0 - d0 - DCH;                   // first staged R column (a multiple of 4)
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const bool active = tid < WQ * DQN;
+  const int wq = tid % WQ, dq = tid / WQ;
   const size_t plane = static_cast<size_t>(H) * W;
-  const int region0 = max(2 * Cg * W, 2 * Cs * W);
-  float* L = smem;
-  float* R = smem + Cg * W;
-  float* gw = smem + region0;            // [G][DC][W]
-  float* Ws = gw + G * DC * W;           // [Cs][G]
-  const int nq = W / VEC;
-  const int items = dn * nq;
-
-  // ---- phase 1: group correlations into LDS
-  for (int g = 0; g < G; ++g) {
-    stage_group(fl, L, b, h, g, Cg, C, H, W);
-    stage_group(fr, R, b, h, g, Cg, C, H, W);
-    for (int it = threadIdx.x; it < items; it += kThreads) {
-      const int dl = it / nq, q = it - dl * nq;
-      const int d = d0 + dl, w0 = q * VEC;
-      float acc[VEC];
-      int ri[VEC];
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        acc[j] = 0.f;
-        ri[j] = max(w0 + j - d, 0);  // clamped in-bounds; invalid lanes zeroed below
-      }
-      for (int c = 0; c < Cg; ++c) {
-        float lv[VEC];
-        load_vec<VEC>(L + c * W + w0, lv);
-        const float* Rc = R + c * W;
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] += lv[j] * Rc[ri[j]];
-      }
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] = (w0 + j >= d) ? acc[j] : 0.f;
-      store_vec<VEC>(gw + (g * DC + dl) * W + w0, acc);
-    }
-    __syncthreads();
-  }
-
-  // ---- phase 2: stage A/Bm rows and the gwc columns of the stem weight, emit Cs channels
   float* As = smem;
-  float* Bs = smem + Cs * W;
-  const float* Ab = A + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
-  const float* Bb = Bm + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W;
-  for (int i = threadIdx.x; i < Cs * nq; i += kThreads) {
-    const int o = i / nq, q = i - o * nq;
-    float va[VEC], vb[VEC];
-    load_vec<VEC>(Ab + o * plane + q * VEC, va);
-    load_vec<VEC>(Bb + o * plane + q * VEC, vb);
-    store_vec<VEC>(As + o * W + q * VEC, va);
-    store_vec<VEC>(Bs + o * W + q * VEC, vb);
-  }
-  for (int i = threadIdx.x; i < Cs * G; i += kThreads) Ws[i] = Wg[i];
-  __syncthreads();
+  float* Bs = As + Cs * WT;
+  float* Ws = Bs + Cs * RS;
+  float* invn = Ws + Cs * G;                       // [G][WT + RS] inverse column norms (L then R)
+  float* grp = invn + G * NC;                      // [GP][Cg][WT] L rows, then [GP][Cg][RS] R rows
+  float* Rg = grp + GP * Cg * WT;
+  const float* flb = fl + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
+  const float* frb = fr + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
+  // R window of this thread: positions base-4 .. base+3 of a staged row, base = 4(wq-dq) + DCH;
+  // output (i, j) (d = d0+4dq+i, w = w0+4wq+j) uses position base + j - i = window slot j - i + 4
+  const int base = 4 * (wq - dq) + DCH;
+  const int wl0 = w0 + 4 * wq, dl0 = d0 + 4 * dq;
+  // dbg bit 2: per-block phase timestamps (wall clock, 100 MHz) of thread 0 into output channel 0
+  unsigned long long* ts = reinterpret_cast<unsigned long long*>(out) + static_cast<size_t>(blockIdx.x) * 16;
+  const bool tsr = (dbg & 4) && tid == 0;
+  if (tsr) ts[0] = wall_clock64();
 
-  for (int it = threadIdx.x; it < items; it += kThreads) {
-    const int dl = it / nq, q = it - dl * nq;
-    const int d = d0 + dl, w0 = q * VEC;
-    float gv[G][VEC];
+  // epilogue operands travel with the first phase
+  build_stage_rows<VEC>(A + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W, plane, Cs, WT, w0, W,
+                        As, tid, nthr);
+  build_stage_rows<VEC>(Bm + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W, plane, Cs, RS, rs0, W,
+                        Bs, tid, nthr);
+  for (int i = tid; i < Cs * G; i += nthr) Ws[i] = Wg[i];
+
+  float gwc[G][4][4];
+  const size_t oplane = static_cast<size_t>(D) * plane;
+  float* dst = out + static_cast<size_t>(b) * Cs * oplane + static_cast<size_t>(dl0) * plane +
+               static_cast<size_t>(h) * W + wl0;
+  const bool wok = wl0 < W && !(dbg & 2);          // dbg bit 1: skip the stores (compute timing)
+
+  // dot products of the thread's 4 d x 4 w outputs for groups [g0, g0 + GP) (staged at slots
+  // 0..GP-1).  Output (i, j) is l_j * r_k, k = j - i + 4 (R window slot).  v_pk_fma_f32 takes
+  // each half of each source from ONE aligned register pair (op_sel picks the halves), so two
+  // outputs share a packed FMA when their l's lie in one of (l0,l1) / (l2,l3) and their r's in
+  // one of (r0,r1) .. (r6,r7): 6 such pairs, all with a broadcast r, cover 12 outputs and the 4
+  // left over are plain FMAs -- 10 VALU per channel, no register shuffles, and both R float4
+  // reads stay whole ds_read_b128s.  (Pairing along w made the compiler re-read R at odd
+  // offsets with ds_read2_b32; pairing through a shifted (l1,l2) pair cost 6 moves a channel.)
+  auto dots = [&](int g0) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) load_vec<VEC>(gw + (g * DC + dl) * W + w0, gv[g]);
-    int bi[VEC];
-    bool ok[VEC];
+    for (int gl = 0; gl < GP; ++gl) {
+      const float* L = grp + gl * Cg * WT + 4 * wq;
+      const float* R = Rg + gl * Cg * RS + base;
+      f2 q10 = 0.f, q20 = 0.f, q00 = 0.f, q12 = 0.f, q22 = 0.f, q02 = 0.f;
+      float s01 = 0.f, s30 = 0.f, s03 = 0.f, s32 = 0.f;
+      const int cend = (dbg & 1) ? 0 : Cg;       // dbg bit 0: skip the dot products (store-path timing)
+      auto step = [&](const f4& l, const f4& ra, const f4& rb) {   // ra: slots 0..3, rb: 4..7
+        const f2 l01 = l.xy, l23 = l.zw;
+        q10 += l01 * ra.ww;                        // (1,0) (2,1)  r3
+        q20 += l01 * ra.zz;                        // (2,0) (3,1)  r2
+        q00 += l01 * rb.xx;                        // (0,0) (1,1)  r4
+        q12 += l23 * rb.yy;                        // (1,2) (2,3)  r5
+        q22 += l23 * rb.xx;                        // (2,2) (3,3)  r4
+        q02 += l23 * rb.zz;                        // (0,2) (1,3)  r6
+        // singles as opaque FMAs: left to itself the SLP vectoriser pairs them through moves
+        asm("v_fmac_f32 %0, %1, %2" : "+v"(s01) : "v"(l.y), "v"(rb.y));   // (0,1) r5
+        asm("v_fmac_f32 %0, %1, %2" : "+v"(s30) : "v"(l.x), "v"(ra.y));   // (3,0) r1
+        asm("v_fmac_f32 %0, %1, %2" : "+v"(s03) : "v"(l.w), "v"(rb.w));   // (0,3) r7
+        asm("v_fmac_f32 %0, %1, %2" : "+v"(s32) : "v"(l.z), "v"(ra.w));   // (3,2) r3
+      };
+      // channels 4 at a time, all 12 LDS reads issued before the FMAs (the asm FMAs block the
+      // compiler's own unrolling); the channel order of every sum is unchanged
+      int c = 0;
+      for (; c + 4 <= cend; c += 4, L += 4 * WT, R += 4 * RS) {
+        f4 l[4], ra[4], rb[4];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      ok[j] = w0 + j >= d;
-      bi[j] = max(w0 + j - d, 0);
-    }
-    float* dst = out + (static_cast<size_t>(b) * Cs * D + d) * plane + static_cast<size_t>(h) * W + w0;
-    for (int o = 0; o < Cs; ++o) {
-      float v[VEC];
-      load_vec<VEC>(As + o * W + w0, v);
-      const float* Bo = Bs + o * W;
-      const float* wo = Ws + o * G;
+        for (int u = 0; u < 4; ++u) {
+          l[u] = *reinterpret_cast<const f4*>(L + u * WT);
+          ra[u] = *reinterpret_cast<const f4*>(R + u * RS - 4);
+          rb[u] = *reinterpret_cast<const f4*>(R + u * RS);
+        }
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int g = 0; g < G; ++g) s += wo[g] * gv[g][j];
-        v[j] = v[j] + (ok[j] ? Bo[bi[j]] : 0.f) + s;
+        for (int u = 0; u < 4; ++u) step(l[u], ra[u], rb[u]);
       }
-      store_vec<VEC>(dst + static_cast<size_t>(o) * D * plane, v);
+      for (; c < cend; ++c, L += WT, R += RS)
+        step(*reinterpret_cast<const f4*>(L), *reinterpret_cast<const f4*>(R - 4), *reinterpret_cast<const f4*>(R));
+      float (&o)[4][4] = gwc[g0 + gl];
+      o[1][0] = q10.x; o[2][1] = q10.y; o[2][0] = q20.x; o[3][1] = q20.y;
+      o[0][0] = q00.x; o[1][1] = q00.y; o[1][2] = q12.x; o[2][3] = q12.y;
+      o[2][2] = q22.x; o[3][3] = q22.y; o[0][2] = q02.x; o[1][3] = q02.y;
+      o[0][1] = s01; o[3][0] = s30; o[0][3] = s03; o[3][2] = s32;
     }
+  };
+  // inverse column norms of groups [g0, g0 + GP): one thread per staged column (idle threads
+  // first) sums all GP groups, so GP x 4 independent LDS reads are in flight per step
+  auto norms = [&](int g0) {
+    for (int col = nthr - 1 - tid; col < NC; col += nthr) {
+      const float* src = col < WT ? grp + col : Rg + (col - WT);
+      const int stride = col < WT ? WT : RS;
+      float ss[GP][4];
+#pragma unroll
+      for (int gl = 0; gl < GP; ++gl)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ss[gl][u] = 0.f;
+      int c = 0;
+      for (; c + 4 <= Cg; c += 4) {
+#pragma unroll
+        for (int gl = 0; gl < GP; ++gl) {
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = src[(gl * Cg + c + u) * stride];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) ss[gl][u] += v[u] * v[u];
+        }
+      }
+      for (; c < Cg; ++c)
+#pragma unroll
+        for (int gl = 0; gl < GP; ++gl) {
+          const float v = src[(gl * Cg + c) * stride];
+          ss[gl][0] += v * v;
+        }
+#pragma unroll
+      for (int gl = 0; gl < GP; ++gl) {
+        const float t = (ss[gl][0] + ss[gl][1]) + (ss[gl][2] + ss[gl][3]);
+        invn[(g0 + gl) * NC + col] = t > 1e-24f ? __builtin_amdgcn_rsqf(t) : 1e12f;   // 1 / max(|x|, 1e-12)
+      }
+    }
+  };
+
+#pragma unroll
+  for (int ph = 0; ph < NPH; ++ph) {
+    if (ph > 0) __syncthreads();                   // previous phase's groups fully consumed
+    build_stage_rows<VEC>(flb + static_cast<size_t>(ph) * GP * Cg * plane, plane, GP * Cg, WT, w0, W, grp, tid, nthr);
+    build_stage_rows<VEC>(frb + static_cast<size_t>(ph) * GP * Cg * plane, plane, GP * Cg, RS, rs0, W, Rg, tid, nthr);
+    __builtin_amdgcn_s_waitcnt(0);                 // this thread's LDS-DMA pieces have landed
+    __syncthreads();
+    if (tsr) ts[1 + 2 * ph] = wall_clock64();
+    norms(ph * GP);
+    if (active) dots(ph * GP);
+    if (tsr) ts[2 + 2 * ph] = wall_clock64();
+  }
+  __syncthreads();                                 // invn complete
+  if (tsr) ts[9] = wall_clock64();
+  if (!active) return;
+  // normalise: gwc *= inv|L|[w] * inv|R|[w - d]
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const f4 il = *reinterpret_cast<const f4*>(invn + g * NC + 4 * wq);
+    const f4 ia = *reinterpret_cast<const f4*>(invn + g * NC + WT + base - 4);
+    const f4 ib = *reinterpret_cast<const f4*>(invn + g * NC + WT + base);
+    const float rv[8] = {ia.x, ia.y, ia.z, ia.w, ib.x, ib.y, ib.z, ib.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gwc[g][i][j] = gwc[g][i][j] * il[j] * rv[j - i + 4];
+  }
+#pragma unroll 2
+  for (int o = 0; o < Cs; ++o) {
+    const f4 av = *reinterpret_cast<const f4*>(As + o * WT + 4 * wq);
+    const f4 ba = *reinterpret_cast<const f4*>(Bs + o * RS + base - 4);
+    const f4 bb = *reinterpret_cast<const f4*>(Bs + o * RS + base);
+    const f4 g0 = *reinterpret_cast<const f4*>(Ws + o * G);
+    const f4 g1 = *reinterpret_cast<const f4*>(Ws + o * G + 4);
+    const float bv[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+    const float wv[G] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    float* po = dst + static_cast<size_t>(o) * oplane;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int g = 0; g < G; ++g) sacc += wv[g] * gwc[g][i][j];
+        v[j] = av[j] + bv[j - i + 4] + sacc;       // Bm staged as 0 left of column 0: the w < d zeros
+      }
+      if (dl0 + i < D && wok && !((dbg & 4) && o == 0)) {   // dbg 4: channel 0 holds the timestamps
+        float* pp = po + static_cast<size_t>(i) * plane;
+        if constexpr (VEC == 4) {
+          *reinterpret_cast<float4*>(pp) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (wl0 + j < W) pp[j] = v[j];
+        }
+      }
+    }
+  }
+  if (tsr) {
+    ts[10] = wall_clock64();
+    __builtin_amdgcn_s_waitcnt(0);
+    ts[11] = wall_clock64();
   }
 }
 
@@ -414,6 +591,67 @@ int launch_gwc(const float* fl, const float* fr, float* out, int B, int C, int G
   return finish_launch("gwc volume");
 }
 
+
+// Single-pass build tile: thread grid WQ column quads x DQN disparity quads (<= 256 threads, one
+// block per CU -- the LDS image is ~130 KB at cfg2 -- so the default aims for at most one block
+// per CU and few column tiles).  Groups are staged in the fewest phases whose LDS image fits the
+// CU's 160 KB.  FSMI_BUILD_TILE = "WQ,DQN" overrides (A/B measurement); FSMI_BUILD_DBG: 1 no dot
+// products, 2 no stores, 4 phase timestamps (tools/build_phases.py).
+int launch_build_stem(const float* fl, const float* fr, const float* A, const float* Bm, const float* Wg, float* out,
+                      int B, int C, int Cs, int D, int H, int W, hipStream_t s) {
+  const int Cg = C / kBuildG;
+  // disparity quads in balanced chunks of at most 16 (cfg2's D4 = 48: one chunk of 12; D4 = 80:
+  // two of 10)
+  const int dq_all = (D + 3) / 4, nchunk = (dq_all + 15) / 16;
+  int DQN = (dq_all + nchunk - 1) / nchunk, WQ = 8;
+  const char* env = std::getenv("FSMI_BUILD_TILE");
+  int ew = 0, ed = 0;
+  if (env && std::sscanf(env, "%d,%d", &ew, &ed) == 2 && ew > 0 && ed > 0 && ew * ed <= kThreads) {
+    WQ = ew;
+    DQN = ed;
+  } else {
+    // widest column tile (fewest column tiles, least R-row overlap) the 256-thread block allows,
+    // then balanced over the row: cfg2 (W4 = 160, D4 = 48) -> 2 tiles of 20 quads, 240 blocks
+    const int wq_max = std::max(1, kThreads / DQN), nq = (W + 3) / 4;
+    const int ntile = (nq + wq_max - 1) / wq_max;
+    WQ = (nq + ntile - 1) / ntile;
+  }
+  const int WT = 4 * WQ, DCH = 4 * DQN, RS = WT + DCH;
+  const int nthr = (WQ * DQN + kWave - 1) / kWave * kWave;
+  int GP = kBuildG;
+  while (GP > 1 && static_cast<size_t>(build_lds_floats(Cg, Cs, WT, RS, GP)) * sizeof(float) > 160 * 1024) GP /= 2;
+  const size_t lds = static_cast<size_t>(build_lds_floats(Cg, Cs, WT, RS, GP)) * sizeof(float);
+  FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_comb_volume_stem: LDS image %zu B too large (C=%d)", lds, C);
+  const int nwt = (W + WT - 1) / WT, ndc = (D + DCH - 1) / DCH;
+  const unsigned grid = static_cast<unsigned>(B) * H * nwt * ndc;
+  const bool vec = (W % 4) == 0;
+  const char* dbs = std::getenv("FSMI_BUILD_DBG");
+  const int dbg = dbs ? std::atoi(dbs) : 0;
+  LaunchTimer t(FSMI_K_COMB, s);
+#define FSMI_BUILD_CASE(V, P)                                                                                     \
+  do {                                                                                                            \
+    const void* fn = reinterpret_cast<const void*>(build_stem_kernel<V, P>);                                      \
+    if (lds > 64 * 1024 &&                                                                                        \
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess) \
+      return finish_launch("fsmi_comb_volume_stem: LDS attribute");                                               \
+    hipLaunchKernelGGL((build_stem_kernel<V, P>), dim3(grid), dim3(nthr), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D, \
+                       H, W, WQ, DQN, nwt, ndc, dbg);                                                             \
+  } while (0)
+  if (vec) {
+    if (GP == 8) FSMI_BUILD_CASE(4, 8);
+    else if (GP == 4) FSMI_BUILD_CASE(4, 4);
+    else if (GP == 2) FSMI_BUILD_CASE(4, 2);
+    else FSMI_BUILD_CASE(4, 1);
+  } else {
+    if (GP == 8) FSMI_BUILD_CASE(1, 8);
+    else if (GP == 4) FSMI_BUILD_CASE(1, 4);
+    else if (GP == 2) FSMI_BUILD_CASE(1, 2);
+    else FSMI_BUILD_CASE(1, 1);
+  }
+#undef FSMI_BUILD_CASE
+  return finish_launch("fsmi_comb_volume_stem");
+}
+
 }  // namespace
 }  // namespace fsmi
 
@@ -464,34 +702,7 @@ int fsmi_comb_volume_stem(const float* fl, const float* fr, const float* A, cons
                          Bm, Wg, out, Cs, D, H, W, total);
     return finish_launch("fsmi_comb_volume_stem");
   }
-  const int Cg = C / G;
-  // largest disparity chunk (<= 8) whose LDS image fits: staging/A-Bm rows + gwc tile + stem columns
-  auto lds_for = [&](int dc) {
-    return (static_cast<size_t>(std::max(2 * Cg * W, 2 * Cs * W)) + static_cast<size_t>(G) * dc * W + Cs * G) *
-           sizeof(float);
-  };
-  int DC = std::min(D, 8);
-  while (DC > 1 && lds_for(DC) > 160 * 1024) DC >>= 1;
-  const size_t lds = lds_for(DC);
-  FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_comb_volume_stem: row too large for LDS (W=%d)", W);
-  const int nDC = (D + DC - 1) / DC;
-  const unsigned grid = static_cast<unsigned>(B) * H * nDC;
-  hipStream_t s = as_stream(stream);
-  const bool vec = (W % 4) == 0;
-  const void* fn = vec ? reinterpret_cast<const void*>(comb_stem_kernel<8, 4>)
-                       : reinterpret_cast<const void*>(comb_stem_kernel<8, 1>);
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    if (e != hipSuccess) return finish_launch("fsmi_comb_volume_stem: LDS attribute");
-  }
-  LaunchTimer t(FSMI_K_COMB, s);
-  if (vec)
-    hipLaunchKernelGGL((comb_stem_kernel<8, 4>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D,
-                       H, W, DC, nDC);
-  else
-    hipLaunchKernelGGL((comb_stem_kernel<8, 1>), dim3(grid), dim3(kThreads), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D,
-                       H, W, DC, nDC);
-  return finish_launch("fsmi_comb_volume_stem");
+  return launch_build_stem(fl, fr, A, Bm, Wg, out, B, C, Cs, D, H, W, as_stream(stream));
 }
 
 int fsmi_pointwise_proj(const float* x, const float* Wt, const float* bias, float* out, int B, int C, int O, int H,

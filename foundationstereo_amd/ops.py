@@ -87,17 +87,18 @@ def pointwise_proj(x: Tensor, wt: Tensor, bias: Tensor = None) -> Tensor:
 
 
 def comb_volume_stem(fl: Tensor, fr: Tensor, A: Tensor, Bm: Tensor, Wg: Tensor, maxdisp: int,
-                     two_pass: bool = True) -> Tensor:
+                     two_pass: bool = False) -> Tensor:
     """Fused gwc + concat + corr_stem[0] (core/foundation_stereo.py:207-213,165) -> (B,Cs,D,H,W).
 
-    ``two_pass`` (default): gwc into a (B,G,D,H,W) scratch then one streaming
-    pass; otherwise a single LDS-staged kernel (no scratch)."""
+    Default: one LDS-staged streaming kernel (no scratch); ``two_pass`` (or
+    FSMI_BUILD_TWO_PASS=1): gwc into a (B,G,D,H,W) scratch, then a stem pass."""
     _check("comb_volume_stem", fl, fr, A, Bm, Wg)
     B, C, H, W = fl.shape
     Cs, G = Wg.shape
     assert C % G == 0, f"C:{C}, num_groups:{G}"
     fl, fr, A, Bm, Wg = _c(fl), _c(fr), _c(A), _c(Bm), _c(Wg)
     out = torch.empty((B, Cs, maxdisp, H, W), device=fl.device, dtype=torch.float32)
+    two_pass = two_pass or os.environ.get("FSMI_BUILD_TWO_PASS", "0") == "1"
     ws = torch.empty((B, G, maxdisp, H, W), device=fl.device, dtype=torch.float32) if two_pass else None
     _lib.check(_lib.load().fsmi_comb_volume_stem(_p(fl), _p(fr), _p(A), _p(Bm), _p(Wg),
                                                  _p(ws) if ws is not None else None, _p(out), B, C, G, Cs,

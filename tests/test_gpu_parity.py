@@ -97,12 +97,36 @@ def test_comb_volume_stem_vs_oracle(ops_mod, vit, W):
         ref = oracle.stereo_oracle._conv(P, "corr_stem.0", comb)
         wg, wa, ba, wb, bb = m._stem_weights()
         A, Bm = ops_mod.pointwise_proj(g(fl), wa, ba), ops_mod.pointwise_proj(g(fr), wb, bb)
-        one_pass = ops_mod.comb_volume_stem(g(fl), g(fr), A, Bm, wg, D, two_pass=False)
+        two_pass = ops_mod.comb_volume_stem(g(fl), g(fr), A, Bm, wg, D, two_pass=True)
         m.fused_volume = False
         unfused = m.build_stem_volume(g(fl), g(fr))
     close(out, ref, atol=2e-5)
-    close(one_pass, ref, atol=2e-5)
+    close(two_pass, ref, atol=2e-5)
     close(unfused, ref, atol=2e-5)
+
+
+@pytest.mark.parametrize("vit,W,D,tile", [("vits", 100, 80, "16,16"), ("vits", 100, 80, "8,12"), ("vitl", 52, 24, "4,6"),
+                                          ("vits", 37, 20, "16,4"), ("vitl", 160, 48, ""), ("vits", 13, 8, "")])
+def test_build_stem_tiles(ops_mod, vit, W, D, tile, monkeypatch):
+    """Single-pass build over tile shapes (ragged column / disparity tiles, several chunks, W % 4 != 0)
+    == the oracle's Conv3d_1x1(cat(gwc, concat(proj(fl), proj(fr)))) (core/foundation_stereo.py:207-213,165)."""
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    monkeypatch.setenv("FSMI_BUILD_TILE", tile)
+    args = synth.make_args(max_disp=4 * D, corr_levels=2, vit_size=vit)
+    m = FoundationStereo(args)
+    synth.init_module_(m, seed=6)
+    m = m.to(DEV).eval()
+    C = m.feature.d_out[0]
+    B, H = 1, 2
+    fl, fr = synth.normal(31, (B, C, H, W)), synth.normal(32, (B, C, H, W))
+    with torch.no_grad():
+        out = m.build_stem_volume(g(fl), g(fr))
+        P = {k: v.cpu() for k, v in m.state_dict().items()}
+        comb = torch.cat([oracle.build_gwc_volume(t(fl), t(fr), D, 8),
+                          oracle.build_concat_volume(oracle.stereo_oracle._conv(P, "proj_cmb", t(fl)),
+                                                     oracle.stereo_oracle._conv(P, "proj_cmb", t(fr)), D)], 1)
+        ref = oracle.stereo_oracle._conv(P, "corr_stem.0", comb)
+    close(out, ref, atol=2e-5)
 
 
 @pytest.mark.parametrize("KS,shape", [(7, (1, 14, 12, 16, 40)), (7, (2, 5, 5, 9, 33)), (3, (1, 14, 8, 8, 64))])
