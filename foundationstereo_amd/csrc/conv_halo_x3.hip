@@ -57,6 +57,7 @@ struct HaloArgs {
   int nrt, nct, npix, nco;         // row tiles, col tiles, pixel tiles (B*D*nrt*nct), cout tiles
   int nsplit, kpc;                 // split-K factor, (kd, channel chunk) pairs per split
   float* ws;                       // [nsplit][B][Cout][D*H*W] partial sums when nsplit > 1
+  unsigned long long* ts;          // debug (fsmi_debug_conv_timestamps): per-block wall-clock stamps
   // SelectiveConvGRU gate epilogues (act 3..5), core/update.py:83-95,117; all (B, gHd, H, W)
   // except gatt (B, 1, H, W)
   const float* gh;                 // hidden state h
@@ -79,28 +80,38 @@ __device__ __forceinline__ float sigm_h(float x) { return 1.f / (1.f + expf(-x))
 //  act 5 (large convq):  out[b,co0+co] += ((1-z)h + z tanh(v + bias)) * (1 - att)
 // RESPRE: compile the res_pre (ResNet tail) path; the 2D conv kernels instantiate without it --
 // with the branch present their epilogue needs ~100 more VGPRs (occupancy 2 -> 1).
-template <bool RESPRE = true>
-__device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, int b, long long hw) {
+// Every tensor arrives as its own __restrict__ parameter: a caller that runs a whole batch of
+// elements inside ONE call of a function taking them so lets the compiler issue all the batch's
+// loads (bias, residual, gate state) ahead of its stores.  Read through the HaloArgs fields
+// (which may alias the output) each load waited behind the previous element's store, and a
+// tile's epilogue paid one L2 round trip per element: 20-56 % of a block's lifetime on the
+// nsplit = 1 layers (tools/conv_phases.py).
+template <bool RESPRE>
+__device__ __forceinline__ void store_el(const HaloArgs& a, float v, int co, int b, long long hw,
+                                         float* __restrict__ out, const float* __restrict__ bias,
+                                         const float* __restrict__ gamma, const float* __restrict__ res,
+                                         const float* __restrict__ gh, float* __restrict__ gz,
+                                         const float* __restrict__ gatt, float* __restrict__ grh) {
   const long long HW = a.cstride;
-  if (a.bias) v += a.bias[co];
+  if (bias) v += bias[co];
   if (a.act >= 3 && a.act <= 5) {
     const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
     if (a.act == 3) {
       const float sg = sigm_h(v);
-      if (co < a.gHd) a.gz[g] = sg;
-      else a.grh[g] = sg * a.gh[g];
+      if (co < a.gHd) gz[g] = sg;
+      else grh[g] = sg * gh[g];
       return;
     }
-    const float z = a.gz[g], hv = a.gh[g], at = a.gatt[static_cast<size_t>(b) * HW + hw];
+    const float z = gz[g], hv = gh[g], at = gatt[static_cast<size_t>(b) * HW + hw];
     const float hn = (1.f - z) * hv + z * tanhf(v);
-    float* o = a.out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+    float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
     if (a.act == 4) *o = hn * at;
     else *o = *o + hn * (1.f - at);
     return;
   }
-  float* o = a.out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+  float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
   if (RESPRE && a.res_pre) {       // ResNet tail: act(v + bias + res)
-    v += a.res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
+    v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
     *o = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v);
     return;
   }
@@ -108,9 +119,81 @@ __device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, in
   else if (a.act == 2) v = gelu_erf_h(v);
   else if (a.act == 6) v = v >= 0.f ? v : 0.01f * v;
   v *= a.alpha;
-  if (a.gamma) v *= a.gamma[co];
-  if (a.res) v += a.res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
+  if (gamma) v *= gamma[co];
+  if (res) v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
   *o = v;
+}
+
+template <bool RESPRE = true>
+__device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, int b, long long hw) {
+  store_el<RESPRE>(a, v, co, b, hw, a.out, a.bias, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh);
+}
+
+// One 16-element accumulator fragment (couts cb + (r&3) + 8(r>>2)) at one pixel, activation ACT
+// fixed at compile time and one restrict scope: the fragment's bias / gamma / residual / gate
+// loads are issued together, then 16 branch-free finishes and stores.  (The generic store_el per
+// element compiled to ~400 instructions per fragment with a wait per element: 20-56 % of a
+// block's lifetime went to the epilogue on the nsplit = 1 layers, tools/conv_phases.py.)
+template <int ACT, bool RESPRE>
+__device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, int cb, int b, long long hw,
+                                           float* __restrict__ out, const float* __restrict__ bias,
+                                           const float* __restrict__ gamma, const float* __restrict__ res,
+                                           const float* __restrict__ gh, float* __restrict__ gz,
+                                           const float* __restrict__ gatt, float* __restrict__ grh) {
+  const long long HW = a.cstride;
+  float bv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bv[r] = bias ? bias[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)] : 0.f;
+  if constexpr (ACT >= 3 && ACT <= 5) {
+    const float at = ACT == 3 ? 0.f : gatt[static_cast<size_t>(b) * HW + hw];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = cb + (r & 3) + 8 * (r >> 2);
+      if (co >= a.Cout) continue;
+      const float x = v[r] * a.wscale + bv[r];
+      const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
+      if constexpr (ACT == 3) {
+        const float sg = sigm_h(x);
+        if (co < a.gHd) gz[g] = sg;
+        else grh[g] = sg * gh[g];
+      } else {
+        const float z = gz[g];
+        const float hn = (1.f - z) * gh[g] + z * tanhf(x);
+        float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+        if constexpr (ACT == 4) *o = hn * at;
+        else *o = *o + hn * (1.f - at);
+      }
+    }
+    return;
+  } else {
+    float gv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gv[r] = gamma ? gamma[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)] : 1.f;
+    const bool pre = RESPRE && a.res_pre;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = cb + (r & 3) + 8 * (r >> 2);
+      if (co >= a.Cout) continue;
+      float x = v[r] * a.wscale + bv[r];
+      const float rv = res ? res[b * a.res_bstride + static_cast<long long>(co) * HW + hw] : 0.f;
+      if (pre) x += rv;            // ResNet tail: act(conv + bias + res)
+      if constexpr (ACT == 1) x = fmaxf(x, 0.f);
+      else if constexpr (ACT == 2) x = gelu_erf_h(x);
+      else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
+      if (!pre) x = x * a.alpha * gv[r] + rv;
+      out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw] = x;
+    }
+  }
+}
+
+// 4 consecutive pixels of one channel, one restrict scope
+__device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], int co, int b, long long hw,
+                                       float* __restrict__ out, const float* __restrict__ bias,
+                                       const float* __restrict__ gamma, const float* __restrict__ res,
+                                       const float* __restrict__ gh, float* __restrict__ gz,
+                                       const float* __restrict__ gatt, float* __restrict__ grh) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) store_el<true>(a, v[k], co, b, hw + k, out, bias, gamma, res, gh, gz, gatt, grh);
 }
 
 // ---------------------------------------------------------------- shared pieces
@@ -243,18 +326,35 @@ __device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM
     }
 }
 
+// Non-split epilogue of the block's tile with the activation fixed at compile time
+template <int ACT, int TM, int TN, bool D3>
+__device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[TM][TN], const TileCoord& t, int wm,
+                                         int wn, int lane) {
+  const int hsel = lane >> 5, rl = lane & 31;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
+    if (hh >= a.H || ww >= a.W) continue;
+    const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      store_frag<ACT, D3>(a, acc[i][j], t.m0 + (wm * TM + i) * 32 + 4 * hsel, t.b, hw, a.out, a.bias, a.gamma, a.res,
+                          a.gh, a.gz, a.gatt, a.grh);
+  }
+}
+
 // n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
 template <int TM, int TN, bool D3>
 __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], const TileCoord& t,
                                               int wm, int wn, int lane) {
   const int hsel = lane >> 5, rl = lane & 31;
   const long long HW = a.cstride;
+  if (a.nsplit > 1) {              // raw partial sums; the split reduce applies the epilogue
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
-    if (hh >= a.H || ww >= a.W) continue;
-    const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
-    if (a.nsplit > 1) {            // raw partial sums; the split reduce applies the epilogue
+    for (int j = 0; j < TN; ++j) {
+      const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
+      if (hh >= a.H || ww >= a.W) continue;
+      const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
       float* wp = a.ws + (static_cast<size_t>(t.split) * a.B + t.b) * a.Cout * HW + hw;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -263,15 +363,17 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
           const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
           if (co < a.Cout) wp[static_cast<size_t>(co) * HW] = acc[i][j][r] * a.wscale;
         }
-      continue;
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-        if (co < a.Cout) store_out<D3>(a, acc[i][j][r] * a.wscale, co, t.b, hw);
-      }
+    return;
+  }
+  switch (a.act) {                 // uniform: one specialised tile epilogue per activation
+    case 1: epi_tile<1, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
+    case 2: epi_tile<2, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
+    case 3: epi_tile<3, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
+    case 4: epi_tile<4, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
+    case 5: epi_tile<5, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
+    case 6: epi_tile<6, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
+    default: epi_tile<0, TM, TN, D3>(a, acc, t, wm, wn, lane); break;
   }
 }
 
@@ -479,8 +581,11 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  unsigned long long* tsb = a.ts ? a.ts + static_cast<size_t>(blockIdx.x) * 40 : nullptr;
+  if (tsb && tid == 0) tsb[0] = wall_clock64();
   auto stage = [&](int cc) {
     __syncthreads();               // every wave is done with the previous chunk's halo
+    if (tsb && tid == 0 && cc - cc_begin < 36) tsb[1 + cc - cc_begin] = wall_clock64();
     hs.store(Xh, Xl, tid);
     if (cc + 1 < cc_end) {
       if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
@@ -503,7 +608,12 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
     stage(cc);
     chunk(std::integral_constant<int, 0>(), cc);
   }
+  if (tsb && tid == 0) tsb[37] = wall_clock64();
   conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane);
+  if (tsb && tid == 0) {
+    tsb[38] = wall_clock64();
+    tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
+  }
 }
 
 // Sums the split-K partials in split order (deterministic) and applies the epilogue.
@@ -553,10 +663,8 @@ __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
         make_float4(r[0], r[1], r[2], r[3]);
     return;
   }
-  store_out(a, v.x, co, b, hw);
-  store_out(a, v.y, co, b, hw + 1);
-  store_out(a, v.z, co, b, hw + 2);
-  store_out(a, v.w, co, b, hw + 3);
+  const float sv[4] = {v.x, v.y, v.z, v.w};
+  store4(a, sv, co, b, hw, a.out, a.bias, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh);
 }
 
 template <int KS, int BM, int TR, int WM>
@@ -601,6 +709,8 @@ int launch_halo(HaloArgs a, hipStream_t s) {
 using namespace fsmi;
 
 namespace {
+
+unsigned long long* g_conv_ts = nullptr;
 
 // Shared host side of both entry points: validates, fills HaloArgs (gate fields preset by the
 // caller), picks tiles and split-K, launches.
@@ -683,6 +793,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   FSMI_CHECK_ARG(a.nsplit == 1 || (ws && per_split * a.nsplit <= ws_floats),
                  "%s: split-K %d needs %lld workspace floats", what, a.nsplit, per_split * a.nsplit);
   a.ws = ws;
+  a.ts = g_conv_ts;
   if (KS == 3) {
     switch (cfg) {
       case 0: return launch_halo<3, 64, 8, 1, false>(a, s);
@@ -708,6 +819,14 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
 }
 
 }  // namespace
+
+// Debug: while buf is non-NULL every halo conv launch records, per block, thread 0's wall clock
+// (100 MHz) at start [0], at each chunk's staging barrier [1..36], before / after the epilogue
+// [37] / [38] and (chunks << 32 | block) [39] into buf[block * 40 ..] (tools/conv_phases.py).
+extern "C" int fsmi_debug_conv_timestamps(unsigned long long* buf) {
+  g_conv_ts = buf;
+  return FSMI_OK;
+}
 
 extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
                                    const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,

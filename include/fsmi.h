@@ -179,6 +179,11 @@ int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* se
  * epilogue.  ws may be NULL when nsplit is 0/1 (or auto: then no split).
  * (A last-arriving-block fixup inside the conv kernel was measured 4x slower:
  * the agent-scope fences it needs flush and invalidate the per-XCD L2.) */
+/* Debug: while buf != NULL, every halo-conv launch stores per-block wall-clock
+ * stamps (100 MHz) into buf[block*40 + 0..39]: start, each chunk's staging
+ * barrier, before/after the epilogue, (chunks << 32 | block).  NULL disables. */
+int fsmi_debug_conv_timestamps(unsigned long long* buf);
+
 int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
                         const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
                         const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
