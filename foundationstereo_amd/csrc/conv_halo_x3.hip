@@ -18,6 +18,7 @@
 // MFMA v_mfma_f32_32x32x16_f16, three per product (lo*hi, hi*lo, hi*hi), fp32
 // accumulation; fragment maps as in conv2d_x3.hip.  Epilogue identical to
 // fsmi_conv2d (bias, ReLU/GELU, alpha, gamma, residual, channel-offset store).
+#include <cstdlib>
 #include <type_traits>
 
 #include "fsmi_common.h"
@@ -58,6 +59,7 @@ struct HaloArgs {
   int nsplit, kpc;                 // split-K factor, (kd, channel chunk) pairs per split
   float* ws;                       // [nsplit][B][Cout][D*H*W] partial sums when nsplit > 1
   unsigned long long* ts;          // debug (fsmi_debug_conv_timestamps): per-block wall-clock stamps
+  int dbg;                         // ablation (FSMI_CONV_DBG): 1 weights from one line, 2 no halo reloads
   // SelectiveConvGRU gate epilogues (act 3..5), core/update.py:83-95,117; all (B, gHd, H, W)
   // except gatt (B, 1, H, W)
   const float* gh;                 // hidden state h
@@ -283,15 +285,11 @@ struct TileCoord {
   int m0, b, d0, r0, c0, split;
 };
 
-// cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
+// Tile t (cout tile = t / npix, pixel tile = t % npix; D3: depth fastest) -> coordinates
 template <int BM, int TR, bool D3>
-__device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
-  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
-  const int cs = item / a.npix;                    // (cout tile, split) pair
-  const int ptile = item - cs * a.npix;
-  const int ctile = cs / a.nsplit;
+__device__ __forceinline__ TileCoord tile_coord(const HaloArgs& a, int ctile, int ptile) {
   TileCoord t;
-  t.split = cs - ctile * a.nsplit;
+  t.split = 0;
   t.m0 = ctile * BM;
   const int per_plane = a.nrt * a.nct;
   int prem;
@@ -310,6 +308,18 @@ __device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
   }
   t.r0 = (prem / a.nct) * TR;
   t.c0 = (prem % a.nct) * 32;
+  return t;
+}
+
+// cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
+template <int BM, int TR, bool D3>
+__device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int cs = item / a.npix;                    // (cout tile, split) pair
+  const int ptile = item - cs * a.npix;
+  const int ctile = cs / a.nsplit;
+  TileCoord t = tile_coord<BM, TR, D3>(a, ctile, ptile);
+  t.split = cs - ctile * a.nsplit;
   return t;
 }
 
@@ -346,10 +356,10 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
 // n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
 template <int TM, int TN, bool D3>
 __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], const TileCoord& t,
-                                              int wm, int wn, int lane) {
+                                              int wm, int wn, int lane, bool partial) {
   const int hsel = lane >> 5, rl = lane & 31;
   const long long HW = a.cstride;
-  if (a.nsplit > 1) {              // raw partial sums; the split reduce applies the epilogue
+  if (partial) {                   // raw partial sums into ws slot t.split; a reduce applies the epilogue
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
@@ -492,7 +502,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
       }
     }
   }
-  conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane);
+  conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane, a.nsplit > 1);
 }
 
 // ---------------------------------------------------------------- cfg 2/3: weights in registers
@@ -509,111 +519,116 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int hsel = lane >> 5, rl = lane & 31;
-  const TileCoord tc = decode_tile<BM, TR, D3>(a);
   const int nck = a.CinP / HKC;
   const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
+  unsigned long long* tsb = a.ts ? a.ts + static_cast<size_t>(blockIdx.x) * 40 : nullptr;
+  if (tsb && tid == 0) tsb[0] = wall_clock64();
 
-  // this lane's A-fragment rows (rows past Cout only feed outputs the epilogue drops:
-  // clamped so every address is mapped, no zeroing needed)
-  int wrow[TM];
+  // one segment: chunks [cc_begin, cc_end) of tile tc; partial: raw sums into ws slot tc.split
+  auto segment = [&](const TileCoord& tc, int cc_begin, int cc_end, bool partial) {
+    // this lane's A-fragment rows (rows past Cout only feed outputs the epilogue drops:
+    // clamped so every address is mapped, no zeroing needed)
+    int wrow[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) wrow[i] = min(tc.m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
-  half8 wf[2][TM][2][2];           // [buffer][i][k half][hi, lo]
-  auto load_wf = [&](auto buf_c, int cc, int tap) {
-    constexpr int buf = decltype(buf_c)::value;
-    const size_t base = D3 ? (static_cast<size_t>((cc / nck) * NTAP + tap) * nck + cc % nck) * a.CoutP * HKC
-                           : (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+    for (int i = 0; i < TM; ++i) wrow[i] = min(tc.m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
+    half8 wf[2][TM][2][2];         // [buffer][i][k half][hi, lo]
+    auto load_wf = [&](auto buf_c, int cc, int tap) {
+      constexpr int buf = decltype(buf_c)::value;
+      size_t base = D3 ? (static_cast<size_t>((cc / nck) * NTAP + tap) * nck + cc % nck) * a.CoutP * HKC
+                       : (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+      if (a.dbg & 1) base = 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
+          wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+        }
+    };
+    HS hs;
+    hs.init(a, tid, tc.r0, tc.c0);
+
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
-        wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
-      }
-  };
-  HS hs;
-  hs.init(a, tid, tc.r0, tc.c0);
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  f32x16 acc[TM][TN];
+    // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
+    auto chunk = [&](auto par_c, int cc) {
+      constexpr int P = decltype(par_c)::value;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int cc_begin = tc.split * a.kpc;
-  const int cc_end = min(nq, cc_begin + a.kpc);
-  // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
-  auto chunk = [&](auto par_c, int cc) {
-    constexpr int P = decltype(par_c)::value;
-#pragma unroll
-    for (int tap = 0; tap < NTAP; ++tap) {
-      const bool last = tap + 1 == NTAP;
-      if (((tap + P) & 1) == 0) {
-        load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
-      } else {
-        load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
-      }
-      // issue the next tap's loads before this tap's MFMAs: unfenced, the scheduler sinks them
-      // below the last MFMA and reuses the current buffer's registers -- a single buffer whose
-      // L2 round trip every tap then waits on
-      __builtin_amdgcn_sched_barrier(0);
-      const int dh = tap / KS, dw = tap % KS;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        half8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          ah[i] = wf[(tap + P) & 1][i][k][0];
-          al[i] = wf[(tap + P) & 1][i][k][1];
+      for (int tap = 0; tap < NTAP; ++tap) {
+        const bool last = tap + 1 == NTAP;
+        if (((tap + P) & 1) == 0) {
+          load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+        } else {
+          load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
         }
+        // issue the next tap's loads before this tap's MFMAs: unfenced, the scheduler sinks them
+        // below the last MFMA and reuses the current buffer's registers -- a single buffer whose
+        // L2 round trip every tap then waits on
+        __builtin_amdgcn_sched_barrier(0);
+        const int dh = tap / KS, dw = tap % KS;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
-          bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][16 * k + 8 * hsel]);
-          bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][16 * k + 8 * hsel]);
+        for (int k = 0; k < 2; ++k) {
+          half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            ah[i] = wf[(tap + P) & 1][i][k][0];
+            al[i] = wf[(tap + P) & 1][i][k][1];
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+            bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][16 * k + 8 * hsel]);
+            bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][16 * k + 8 * hsel]);
+          }
+          mma3<TM, TN>(acc, ah, al, bh, bl);
         }
-        mma3<TM, TN>(acc, ah, al, bh, bl);
+        // keep the one-tap-ahead structure: without this fence the scheduler hoists every
+        // tap's loads of the unrolled chunk to its top (500 registers, 1 wave per SIMD)
+        __builtin_amdgcn_sched_barrier(0);
       }
-      // keep the one-tap-ahead structure: without this fence the scheduler hoists every
-      // tap's loads of the unrolled chunk to its top (500 registers, 1 wave per SIMD)
-      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto stage = [&](int cc) {
+      __syncthreads();             // every wave is done with the previous chunk's halo
+      if (tsb && tid == 0 && cc - cc_begin < 36) tsb[1 + cc - cc_begin] = wall_clock64();
+      hs.store(Xh, Xl, tid);
+      if (cc + 1 < cc_end && !(a.dbg & 2)) {
+        if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
+        else hs.load(a, tc.b, cc + 1);
+      }   // in flight during this chunk's taps
+      __syncthreads();
+    };
+    load_wf(std::integral_constant<int, 0>(), cc_begin, 0);
+    if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
+    else hs.load(a, tc.b, cc_begin);
+    // chunks in pairs so every register-buffer index is static (parity 0, then 1)
+    int cc = cc_begin;
+    for (; cc + 1 < cc_end; cc += 2) {
+      stage(cc);
+      chunk(std::integral_constant<int, 0>(), cc);
+      stage(cc + 1);
+      chunk(std::integral_constant<int, 1>(), cc + 1);
+    }
+    if (cc < cc_end) {
+      stage(cc);
+      chunk(std::integral_constant<int, 0>(), cc);
+    }
+    if (tsb && tid == 0) tsb[37] = wall_clock64();
+    conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane, partial);
+    if (tsb && tid == 0) {
+      tsb[38] = wall_clock64();
+      tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
     }
   };
-  unsigned long long* tsb = a.ts ? a.ts + static_cast<size_t>(blockIdx.x) * 40 : nullptr;
-  if (tsb && tid == 0) tsb[0] = wall_clock64();
-  auto stage = [&](int cc) {
-    __syncthreads();               // every wave is done with the previous chunk's halo
-    if (tsb && tid == 0 && cc - cc_begin < 36) tsb[1 + cc - cc_begin] = wall_clock64();
-    hs.store(Xh, Xl, tid);
-    if (cc + 1 < cc_end) {
-      if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
-      else hs.load(a, tc.b, cc + 1);
-    }   // in flight during this chunk's taps
-    __syncthreads();
-  };
-  load_wf(std::integral_constant<int, 0>(), cc_begin, 0);
-  if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
-  else hs.load(a, tc.b, cc_begin);
-  // chunks in pairs so every register-buffer index is static (parity 0, then 1)
-  int cc = cc_begin;
-  for (; cc + 1 < cc_end; cc += 2) {
-    stage(cc);
-    chunk(std::integral_constant<int, 0>(), cc);
-    stage(cc + 1);
-    chunk(std::integral_constant<int, 1>(), cc + 1);
-  }
-  if (cc < cc_end) {
-    stage(cc);
-    chunk(std::integral_constant<int, 0>(), cc);
-  }
-  if (tsb && tid == 0) tsb[37] = wall_clock64();
-  conv_epilogue<TM, TN, D3>(a, acc, tc, wm, wn, lane);
-  if (tsb && tid == 0) {
-    tsb[38] = wall_clock64();
-    tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
-  }
+
+  const TileCoord tc = decode_tile<BM, TR, D3>(a);
+  const int c0 = tc.split * a.kpc;
+  segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
 }
 
 // Sums the split-K partials in split order (deterministic) and applies the epilogue.
@@ -677,8 +692,8 @@ void tile_counts(HaloArgs& a) {
 
 template <int KS, int BM, int TR, int WM, bool WREG>
 int launch_halo(HaloArgs a, hipStream_t s) {
-  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
   const bool d3 = a.D > 1 || a.KD > 1;
+  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
   if constexpr (WREG) {
     if (d3) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, true>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, false>), dim3(grid), dim3(256), 0, s, a);
@@ -794,6 +809,11 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
                  "%s: split-K %d needs %lld workspace floats", what, a.nsplit, per_split * a.nsplit);
   a.ws = ws;
   a.ts = g_conv_ts;
+  static const int conv_dbg = [] {
+    const char* e = std::getenv("FSMI_CONV_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.dbg = conv_dbg;
   if (KS == 3) {
     switch (cfg) {
       case 0: return launch_halo<3, 64, 8, 1, false>(a, s);
