@@ -75,7 +75,11 @@ def load():
                         "(run `python -m foundationstereo_amd.build`)")
     lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and name.startswith("fsmi_debug_"):   # debug hooks absent from an older A/B build
+            continue
+        if fn is None:
+            raise FsmiError(f"{path}: missing symbol {name}")
         fn.argtypes = argtypes
         fn.restype = ctypes.c_char_p if name in ("fsmi_last_error", "fsmi_arch") else ctypes.c_int
     _lib = lib

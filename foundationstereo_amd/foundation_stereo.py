@@ -222,6 +222,11 @@ class FoundationStereo(nn.Module):
         disp_preds = []
         disp_up = None
         overlap = _update.OVERLAP and not mp and _update._fast(disp)
+        if overlap and test_mode and self.args.n_gru_layers == 3 and iters > 0 and _update.PIPELINE:
+            # gru16 / gru08 one iteration ahead on their own stream (same math, see run_pipelined)
+            net_list, mask_feat_4, disp = self.update_block.run_pipelined(net_list, inp_list, geo_fn,
+                                                                          disp.detach(), att, iters)
+            return self.upsample_disp(disp, mask_feat_4, stem_2x)
         for itr in range(iters):
             disp = disp.detach()
             if overlap:    # lookup + motion encoder on a side stream beside gru16/gru08 (same math)

@@ -30,6 +30,10 @@ CONV_ENGINE = "fsmi"
 # A/B knobs (default on): motion path on a side stream; GRU gates in the conv epilogues
 OVERLAP = os.environ.get("FSMI_OVERLAP", "1") != "0"
 FUSED_GATES = os.environ.get("FSMI_FUSED_GATES", "1") != "0"
+# gru16 / gru08 pipelined one iteration ahead (BasicSelectiveMultiUpdateBlock.run_pipelined);
+# PIPE_BRANCH: gru04's small branch on its own stream there
+PIPELINE = os.environ.get("FSMI_PIPELINE", "1") != "0"
+PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 
 
 def _fast(x) -> bool:
@@ -57,11 +61,22 @@ _SIDE = {}
 
 
 def _side_stream(device, idx=0):
-    """Side stream ``idx`` of ``device`` (0: motion path, 1: GRU small branch / mask head)."""
+    """Side stream ``idx`` of ``device`` (0: motion path, 1: GRU small branches / mask head, 3: the
+    gru16 / gru08 pipeline of ``run_pipelined``)."""
     s = _SIDE.get((device, idx))
     if s is None:
         s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device)
     return s
+
+
+# side stream the SelectiveConvGRU small branch forks to (1); 0: the branches run in order on the
+# caller's stream (run_pipelined, whose capture must stay within the box's GPU_MAX_HW_QUEUES = 4
+# streams: a capture spread over more crashed hipGraph instantiation)
+_BRANCH = [1]
+
+
+def _branch_stream(device):
+    return _side_stream(device, _BRANCH[0])
 
 
 def _conv(mods, segs, act=None, **kw):
@@ -233,11 +248,11 @@ class SelectiveConvGRU(nn.Module):
                 pk, b = _packed(gru.convq)
                 return pk, b, z, rh
 
-            if OVERLAP:
+            if OVERLAP and _BRANCH[0]:
                 # small (1x1) branch on a side stream beside the large branch's zr conv; the
                 # large blend adds into ``out`` after the small blend has written it
                 main = torch.cuda.current_stream(h.device)
-                side = _side_stream(h.device, 1)
+                side = _branch_stream(h.device)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     pk, b, z, rh = branch(self.small_gru, "blend_small")
@@ -332,6 +347,64 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         delta_disp = self.disp_head(net[0])
         main.wait_stream(side1)
         return net, mask, delta_disp
+
+    def run_pipelined(self, net, inp, geo_fn, disp, att, iters):
+        """``iters`` refinement iterations (``disp += forward(net, inp, geo_fn(disp), disp, att)[2]``
+        each) with gru16 / gru08 running one iteration ahead on a stream of their own.
+
+        gru16(t+1) needs only net[1](t) and net[2](t), so it runs beside gru04(t) and the heads;
+        gru08(t+1) needs net[0](t), so it starts as soon as gru04(t) is done, beside the disparity
+        head and the motion path of t+1 (lookup + encoder, on the motion stream, which need only
+        disp(t+1)).  The critical path per iteration is gru04 + max(head + motion, gru08) instead of
+        gru16 + gru08 + gru04 + head.  Every value is computed by the same kernels from the same
+        inputs as ``forward`` (bit-identical); only the order of independent work changes.
+        One pipeline stream and whole-stream joins: ``main.wait_stream(s_gru)`` is issued after
+        gru08(t) and before gru16(t+1) is enqueued, so gru04(t) waits for the former only.  The
+        mask head shares the motion stream.  A tensor read on another stream is freed only after
+        the freeing stream has joined the reader, so the caching allocator never recycles memory
+        a pending kernel still reads.  Returns (net, mask, disp); mask is the last iteration's."""
+        dev = disp.device
+        main = torch.cuda.current_stream(dev)
+        s_mot, s_gru = _side_stream(dev, 0), _side_stream(dev, 3)
+        n0, n1, n2 = net
+        B, _, H, W = disp.shape
+        main_branch = PIPE_BRANCH                        # gru04's small branch on stream 1 (4th stream)
+        s_gru.wait_stream(main)
+        _BRANCH[0] = 0                                   # pipeline-stream GRUs: branches in order
+        with torch.cuda.stream(s_gru):
+            n2 = self.gru16(att[2], n2, inp[2], pool2x(n1))
+            n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1))
+        _BRANCH[0] = 1
+        mask = None
+        for t in range(iters):
+            enc = disp.new_empty(B, self.encoder.conv.out_channels + 1, H, W)   # on main
+            s_mot.wait_stream(main)
+            with torch.cuda.stream(s_mot):
+                self.encoder.encode_into(disp, geo_fn(disp), enc)
+            main.wait_stream(s_gru)                      # gru08(t): enqueued last on s_gru so far
+            main.wait_stream(s_mot)                      # motion(t)
+            if t + 1 < iters:
+                _BRANCH[0] = 0
+                with torch.cuda.stream(s_gru):           # gru16(t+1), beside gru04(t)
+                    n2 = self.gru16(att[2], n2, inp[2], pool2x(n1))
+                _BRANCH[0] = 1
+            _BRANCH[0] = 1 if main_branch else 0
+            n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0))
+            _BRANCH[0] = 1
+            if t + 1 < iters:
+                s_gru.wait_stream(main)                  # gru04(t)
+                _BRANCH[0] = 0
+                with torch.cuda.stream(s_gru):           # gru08(t+1), beside the heads + motion(t+1)
+                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1))
+                _BRANCH[0] = 1
+            s_mot.wait_stream(main)
+            with torch.cuda.stream(s_mot):
+                mask = _conv(self.mask[2], [_conv(self.mask[0], [n0], "relu")], "relu", alpha=0.25)
+            delta = self.disp_head(n0)
+            main.wait_stream(s_mot)
+            disp = disp + delta.float()
+        main.wait_stream(s_gru)
+        return [n0, n1, n2], mask, disp
 
     def _forward_fast(self, net, inp, corr, disp, att):
         n = self.args.n_gru_layers
