@@ -204,13 +204,14 @@ def main():
     C = synth.feature_dims(vit)[0][0]
     cb_bytes = build_bytes(bl, C, H4, W4, D4)
     cb_avg = (cb_ms / 1e3) / max(cb_n, 1)
-    traffic = None
+    traffic = traffic_build = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_lookup_summary.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
         if pmc.get("config") == a.config and pmc.get("corr_levels") == L:
             traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_build = pmc.get("build_hbm_bytes_per_launch")
 
     pairs = a.steps * B
     res = {
@@ -246,6 +247,7 @@ def main():
         "roofline_build": {"kernel": "comb_volume_stem", "bound": "hbm",
                            "achieved": cb_bytes / cb_avg / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
                            "unit": "GB/s", "frac": cb_bytes / cb_avg / HBM_PEAK if cb_n else None,
+                           "traffic": traffic_build,
                            "algorithmic_bytes": cb_bytes, "avg_us": cb_avg * 1e6, "launches": cb_n},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

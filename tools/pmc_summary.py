@@ -48,6 +48,8 @@ summary = {"config": a.config, "corr_levels": a.corr_levels,
            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), {a.round_dir}",
            "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), KB -> B x1024",
            "hbm_bytes_per_launch": rows[lk[0]]["hbm_bytes_per_launch"] if lk else None,
+           "build_hbm_bytes_per_launch": next((v["hbm_bytes_per_launch"] for k, v in rows.items()
+                                               if k.startswith("build_stem_kernel")), None),
            "kernels": rows}
 os.makedirs(os.path.dirname(a.out), exist_ok=True)
 with open(a.out, "w") as fh:
