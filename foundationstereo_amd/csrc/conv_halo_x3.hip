@@ -690,11 +690,15 @@ void tile_counts(HaloArgs& a) {
   a.nco = (a.Cout + BM - 1) / BM;
 }
 
-template <int KS, int BM, int TR, int WM, bool WREG>
+// D3OK false: 2D-only tile (its volume variant spills -- 464 B/lane for 128x8x32 -- and faulted)
+template <int KS, int BM, int TR, int WM, bool WREG, bool D3OK = true>
 int launch_halo(HaloArgs a, hipStream_t s) {
   const bool d3 = a.D > 1 || a.KD > 1;
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
-  if constexpr (WREG) {
+  if constexpr (WREG && !D3OK) {
+    FSMI_CHECK_ARG(!d3, "fsmi_conv_halo: tile %dx%dx32 is 2D only", BM, TR);
+    hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, false>), dim3(grid), dim3(256), 0, s, a);
+  } else if constexpr (WREG) {
     if (d3) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, true>), dim3(grid), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, false>), dim3(grid), dim3(256), 0, s, a);
   } else {
@@ -781,13 +785,15 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     else if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
     else cfg = Cout > 64 ? 4 : 5;
   }
-  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 7, "%s: cfg %d (0..7)", what, cfg);
+  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 9, "%s: cfg %d (0..9)", what, cfg);
   switch (cfg) {                                  // tile = couts x (rows x 32 px)
     case 0: case 2: tile_counts<3, 64, 8, 1>(a); break;
     case 1: case 3: tile_counts<3, 128, 4, 2>(a); break;
     case 4: tile_counts<3, 128, 2, 2>(a); break;
     case 5: tile_counts<3, 64, 4, 1>(a); break;
     case 6: tile_counts<3, 32, 8, 1>(a); break;
+    case 8: tile_counts<3, 128, 8, 2>(a); break;
+    case 9: tile_counts<3, 256, 4, 4>(a); break;
     default: tile_counts<3, 32, 4, 1>(a); break;
   }
   const int nck = KD * a.CinP / HKC;               // split-K runs over (kd, channel chunk) pairs
@@ -823,6 +829,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
       case 4: return launch_halo<3, 128, 2, 2, true>(a, s);
       case 5: return launch_halo<3, 64, 4, 1, true>(a, s);
       case 6: return launch_halo<3, 32, 8, 1, true>(a, s);
+      case 8: return launch_halo<3, 128, 8, 2, true, false>(a, s);
+      case 9: return launch_halo<3, 256, 4, 4, true, false>(a, s);
       default: return launch_halo<3, 32, 4, 1, true>(a, s);
     }
   }
@@ -834,6 +842,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     case 4: return launch_halo<1, 128, 2, 2, true>(a, s);
     case 5: return launch_halo<1, 64, 4, 1, true>(a, s);
     case 6: return launch_halo<1, 32, 8, 1, true>(a, s);
+    case 8: return launch_halo<1, 128, 8, 2, true, false>(a, s);
+    case 9: return launch_halo<1, 256, 4, 4, true, false>(a, s);
     default: return launch_halo<1, 32, 4, 1, true>(a, s);
   }
 }

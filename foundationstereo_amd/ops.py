@@ -408,7 +408,8 @@ def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Te
 
 # ---- measured tile / split-K choices per conv shape (tools/tune_conv.py -> tuning/fsmi_conv.json):
 # consulted when a caller leaves cfg / nsplit on auto; shapes not in the table use the C-side policy
-_TUNE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "fsmi_conv.json")
+_TUNE_PATH = os.environ.get("FSMI_TUNE_PATH") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "fsmi_conv.json")
 _TUNE = None
 _RECORD = None          # set of shape keys while tools/tune_conv.py records a forward
 

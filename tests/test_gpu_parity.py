@@ -172,10 +172,10 @@ def test_conv2d_mfma_vs_torch(ops_mod, mode, cfg, k, cout, act):
 
 @pytest.mark.parametrize("HW", [(19, 45), (12, 40)])
 @pytest.mark.parametrize("nsplit", [1, 2])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 8, 9])
 @pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (3, 136, None), (1, 129, "relu")])
 def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
-    """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2-5 in registers): 2 segments (16 channels + a 29-channel slice -> 2 channel
+    """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2-5, 8, 9 in registers): 2 segments (16 channels + a 29-channel slice -> 2 channel
     chunks, ragged last chunk), ragged row/column tiles (19x45; 12x40 takes the float4 split-K
     reduce), ragged couts, output slice, every epilogue term, with and without split-K; vs fp64
     torch.  Same 2e-5 abs + 1e-5 rel tolerance as the im2col kernels."""
@@ -196,6 +196,16 @@ def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
     ref = t(res).double() + t(gamma).double().view(1, -1, 1, 1) * 0.75 * y
     close(out[:, 2:2 + cout], ref, atol=2e-5, rtol=1e-5)
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
+
+
+@pytest.mark.gpu
+def test_conv3d_rejects_2d_only_tiles(ops_mod):
+    """cfg 8 / 9 are 2D-only tiles: a volume conv asking for them gets an error, not a launch."""
+    x = torch.zeros(1, 8, 4, 6, 8, device=DEV)
+    pk = ops_mod.PackedConv(torch.zeros(32, 8, 3, 3, 3, device=DEV), mode="halo")
+    for cfg in (8, 9):
+        with pytest.raises(RuntimeError):
+            ops_mod.conv3d(x, pk, cfg=cfg, nsplit=1)
 
 
 @pytest.mark.parametrize("cfg", [-1, 5, 6, 7])

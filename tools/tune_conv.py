@@ -23,6 +23,8 @@ from foundationstereo_amd import ops, synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="cfg2")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--only-cfgs", type=int, nargs="*", default=None,
+                help="time only these cfgs (plus the current table entry); keep the better")
 ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
 a = ap.parse_args()
 dev = torch.device("cuda:0")
@@ -64,6 +66,10 @@ def timeit(fn):
     return e0.elapsed_time(e1) * 1e3 / a.reps
 
 
+prev = {}
+if os.path.exists(ops._TUNE_PATH):
+    with open(ops._TUNE_PATH) as f:
+        prev = json.load(f).get("entries", {})
 entries = {}
 t_start = time.time()
 with torch.no_grad():
@@ -84,10 +90,16 @@ with torch.no_grad():
             return ops.conv3d(x, pk, bias=b, act="relu", cfg=cfg, nsplit=ns)
 
         nck = kd * ((cin + 31) // 32)
-        cfgs = [2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
+        cfgs = ([2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
+                + ([8] if cout > 64 and x.dim() == 4 else []) + ([9] if cout > 128 and x.dim() == 4 else []))
         splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck)]
         auto = timeit(lambda: run(-1, -1))
         best = (auto, -1, -1)
+        if a.only_cfgs is not None:
+            cfgs = [c for c in cfgs if c in a.only_cfgs]
+            old = prev.get(key)
+            if old is not None:
+                best = (timeit(lambda: run(old["cfg"], old["nsplit"])), old["cfg"], old["nsplit"])
         for c in cfgs:
             for s in splits:
                 t = timeit(lambda: run(c, s))
