@@ -48,6 +48,10 @@ SIGNATURES = {
                             ctypes.c_longlong, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_dt_layer_floats": [],
+    "fsmi_dt_patch_embed": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_disparity_transformer": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P],
+    "fsmi_upsample4_add": [_P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_debug_conv_timestamps": [_P],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
@@ -55,7 +59,7 @@ SIGNATURES = {
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
-           "gru_reset", "gru_blend", "conv3d", "conv2d", "dwconv", "resize"]
+           "gru_reset", "gru_blend", "conv3d", "conv2d", "dwconv", "resize", "dt"]
 
 _lib = None
 

@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from . import submodule as _sub
 from . import update as _update
 from .extractor import ContextNetDino, SyntheticFeature
 from .geometry import Combined_Geo_Encoding_Volume
@@ -103,9 +104,37 @@ class hourglass(nn.Module):
         c2 = self.feature_att_up_16(self.agg_0(torch.cat((self.conv3_up(c3), c2), dim=1)), features[2])
         c1 = self.feature_att_up_8(self.agg_1(torch.cat((self.conv2_up(c2), c1), dim=1)), features[1])
         conv = self.conv1_up(c1)
+        if self._dt_fast(x, conv):
+            # patch embed, transformer and the x4 trilinear add on HIP (csrc/transformer.hip)
+            scale, shift = self._patch_fold()
+            t = self.atts["4"](ops.dt_patch_embed(x, self.conv_patch[0].weight, scale, shift))
+            return self.conv_out(ops.upsample4_add_(conv.contiguous(), t))
         t = self.atts["4"](self.conv_patch(x))
         conv = conv + F.interpolate(t, scale_factor=4, mode="trilinear", align_corners=False)
         return self.conv_out(conv)
+
+    def _dt_fast(self, x, conv) -> bool:
+        pc, bn = self.conv_patch[0], self.conv_patch[1]
+        return (x.is_cuda and x.dtype == torch.float32 and conv.dtype == torch.float32 and not self.training
+                and not torch.is_grad_enabled() and not torch.is_autocast_enabled() and _sub.DT_FAST
+                and pc.groups == pc.in_channels == pc.out_channels and pc.kernel_size == (4, 4, 4)
+                and pc.stride == (4, 4, 4) and pc.padding == (0, 0, 0) and bn.track_running_stats
+                and all(n % 4 == 0 for n in x.shape[2:]) and tuple(conv.shape) == tuple(x.shape))
+
+    def _patch_fold(self):
+        """conv_patch bias + eval BatchNorm3d as per-channel (scale, shift), cached per version."""
+        pc, bn = self.conv_patch[0], self.conv_patch[1]
+        ts = [pc.weight, pc.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+        key = tuple((t.data_ptr(), t._version) for t in ts if t is not None)
+        hit = self.__dict__.get("_fsmi_patch")
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                inv = (bn.running_var.double() + bn.eps).rsqrt() * (bn.weight.double() if bn.weight is not None else 1)
+                b = pc.bias.double() if pc.bias is not None else torch.zeros_like(inv)
+                shift = (b - bn.running_mean.double()) * inv + (bn.bias.double() if bn.bias is not None else 0)
+                hit = (key, inv.float().contiguous(), shift.float().contiguous())
+            self.__dict__["_fsmi_patch"] = hit
+        return hit[1], hit[2]
 
 
 class FoundationStereo(nn.Module):

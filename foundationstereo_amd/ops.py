@@ -522,6 +522,71 @@ def resize_bilinear(x: Tensor, size) -> Tensor:
     return out
 
 
+# ---------------------------------------------------------------- disparity transformer
+
+def dt_patch_embed(x: Tensor, w: Tensor, scale: Tensor, shift: Tensor) -> Tensor:
+    """``conv_patch`` (core/foundation_stereo.py:85-88): depthwise Conv3d k4 s4 with bias + eval
+    BatchNorm folded into per-channel ``scale`` / ``shift``; (B,C,D,H,W) -> (B,C,D/4,H/4,W/4)."""
+    _check("dt_patch_embed", x, w, scale, shift)
+    B, C, D, H, W = x.shape
+    assert tuple(w.shape) == (C, 1, 4, 4, 4) and scale.numel() == C and shift.numel() == C
+    x, w, scale, shift = _c(x), _c(w), _c(scale), _c(shift)
+    out = torch.empty((B, C, D // 4, H // 4, W // 4), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_dt_patch_embed(_p(x), _p(w), _p(scale), _p(shift), _p(out), B, C, D, H, W,
+                                               _stream(x)), "dt_patch_embed")
+    return out
+
+
+def dt_layer_floats() -> int:
+    return _lib.load().fsmi_dt_layer_floats()
+
+
+def pack_dt_layers(layers) -> Tensor:
+    """Per-layer parameters of FlashAttentionTransformerEncoderLayer modules in the kernel's
+    order [Wq bq Wk bk Wv bv Wo bo ln1.w ln1.b W1 b1 W2 b2 ln2.w ln2.b]."""
+    parts = []
+    for m in layers:
+        a = m.self_attn
+        for t in (a.q_proj.weight, a.q_proj.bias, a.k_proj.weight, a.k_proj.bias, a.v_proj.weight, a.v_proj.bias,
+                  a.out_proj.weight, a.out_proj.bias, m.norm1.weight, m.norm1.bias, m.linear1.weight,
+                  m.linear1.bias, m.linear2.weight, m.linear2.bias, m.norm2.weight, m.norm2.bias):
+            parts.append(t.detach().float().reshape(-1))
+    p = torch.cat(parts).contiguous()
+    if layers and p.numel() != len(layers) * dt_layer_floats():
+        raise RuntimeError(f"pack_dt_layers: {p.numel()} floats, kernel expects {dt_layer_floats()} per layer "
+                           "(built for d_model 28, 4 heads, FFN 28)")
+    return p
+
+
+def disparity_transformer(x: Tensor, params: Tensor, pe: Tensor, nheads: int, ffdim: int, nlayers: int,
+                          eps: float = 1e-5) -> Tensor:
+    """CostVolumeDisparityAttention.forward (core/submodule.py:506-528) on (B,C,L,H,W): tokens
+    are the L disparities of each pixel; ``pe`` (L, C) is the positional table already sliced."""
+    _check("disparity_transformer", x, params, pe)
+    B, C, L, H, W = x.shape
+    assert tuple(pe.shape) == (L, C)
+    x, params, pe = _c(x), _c(params), _c(pe)
+    out = torch.empty_like(x)
+    _lib.check(_lib.load().fsmi_disparity_transformer(_p(x), _p(out), _p(params), _p(pe), B, C, L, H * W, nheads,
+                                                      ffdim, nlayers, float(eps), _stream(x)),
+               "disparity_transformer")
+    return out
+
+
+def upsample4_add_(vol: Tensor, t: Tensor) -> Tensor:
+    """``vol += F.interpolate(t, scale_factor=4, mode="trilinear", align_corners=False)`` in place
+    (core/foundation_stereo.py:119-120)."""
+    _check("upsample4_add_", vol, t)
+    B, C, D, H, W = t.shape
+    if tuple(vol.shape) != (B, C, 4 * D, 4 * H, 4 * W):
+        raise RuntimeError(f"upsample4_add_: volume {tuple(vol.shape)} is not 4x {tuple(t.shape)}")
+    if not vol.is_contiguous() or vol.data_ptr() % 16:
+        raise RuntimeError("upsample4_add_: the volume must be contiguous and 16-B aligned (in-place add)")
+    t = _c(t)
+    _lib.check(_lib.load().fsmi_upsample4_add(_p(t), _p(vol), B, C, D, H, W, _stream(vol)), "upsample4_add_")
+    return vol
+
+
 # ---------------------------------------------------------------- timing
 
 # algorithmic fp32 conv FLOPs (2*Cin*Cout*k*k*B*H*W) of the conv2d calls made since the last

@@ -49,6 +49,7 @@ class LayerNorm2d(nn.LayerNorm):
 
 
 FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
+DT_FAST = os.environ.get("FSMI_DT", "1") != "0"      # disparity transformer on csrc/transformer.hip
 
 
 def _fast3d(x, conv, bn) -> bool:
@@ -439,8 +440,38 @@ class CostVolumeDisparityAttention(nn.Module):
                                  for _ in range(num_transformer)])
         self.pos_embed0 = PositionalEmbedding(d_model, max_len=max_len)
 
+    def _fast(self, cv) -> bool:
+        if not (DT_FAST and cv.is_cuda and cv.dtype == torch.float32 and not torch.is_grad_enabled()
+                and not torch.is_autocast_enabled()) or self.training:
+            return False
+        a = self.sa[0].self_attn if len(self.sa) else None
+        return (a is not None and cv.shape[1] == 28 and a.num_heads == 4 and self.sa[0].linear1.out_features == 28
+                and type(self.sa[0].act) is nn.GELU and self.sa[0].act.approximate == "none"
+                and 1 <= cv.shape[2] <= 64 and all(m.norm1.eps == m.norm2.eps == self.sa[0].norm1.eps
+                                                   for m in self.sa))
+
+    def _packed(self):
+        ts = [t for m in self.sa for t in m.parameters()]
+        key = tuple((t.data_ptr(), t._version) for t in ts)
+        hit = self.__dict__.get("_fsmi_pack")
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                hit = (key, ops.pack_dt_layers(list(self.sa)))
+            self.__dict__["_fsmi_pack"] = hit
+        return hit[1]
+
     def forward(self, cv, window_size=(-1, -1)):
         B, C, D, H, W = cv.shape
+        if self._fast(cv):
+            # one HIP kernel for PE + all encoder layers (csrc/transformer.hip)
+            pe = self.pos_embed0.pe.to(cv.device, cv.dtype)
+            self.pos_embed0.pe = pe
+            if pe.shape[1] < D:
+                if not self.resize_embed:
+                    raise RuntimeError(f"x:{(B * H * W, D, C)}, pe:{tuple(pe.shape)}")
+                pe = F.interpolate(pe.permute(0, 2, 1), size=D, mode="linear", align_corners=False).permute(0, 2, 1)
+            eps = self.sa[0].norm1.eps
+            return ops.disparity_transformer(cv, self._packed(), pe[0, :D].contiguous(), 4, 28, len(self.sa), eps)
         x = cv.permute(0, 3, 4, 2, 1).reshape(B * H * W, D, C)
         x = self.pos_embed0(x, resize_embed=self.resize_embed)
         for layer in self.sa:

@@ -229,6 +229,28 @@ int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out,
                   int H, int W, void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 
+/* ---- disparity transformer of the hourglass ---------
+ * fsmi_dt_patch_embed: conv_patch = depthwise Conv3d(C, C, 4, stride 4) + eval
+ *   BatchNorm3d (core/foundation_stereo.py:85-88) with bias and BN folded into
+ *   per-channel scale / shift; x (B,C,D,H,W) -> out (B,C,D/4,H/4,W/4); w (C,4,4,4).
+ * fsmi_disparity_transformer: CostVolumeDisparityAttention.forward
+ *   (core/submodule.py:506-528): tokens = the L disparities of each (b,h,w),
+ *   x + pe[:L], then nlayers post-norm encoder layers (core/submodule.py:233-257;
+ *   attention = FlashMultiheadAttention, :198-229, non-causal, scale 1/sqrt(C/nheads),
+ *   FFN with exact GELU, LayerNorm eps).  x, out (B,C,L,HW) NCDHW; pe (L,C);
+ *   params = nlayers x fsmi_dt_layer_floats() floats, each layer
+ *   [Wq bq Wk bk Wv bv Wo bo ln1.w ln1.b W1 b1 W2 b2 ln2.w ln2.b] (Linear weights
+ *   (out,in) row-major).  Built for C=28, 4 heads, FFN 28, L <= 64.
+ * fsmi_upsample4_add: vol (B,C,4D,4H,4W) += F.interpolate(t, scale_factor=4,
+ *   mode="trilinear", align_corners=False) of t (B,C,D,H,W)
+ *   (core/foundation_stereo.py:119-120). */
+int fsmi_dt_layer_floats(void);
+int fsmi_dt_patch_embed(const float* x, const float* w, const float* scale, const float* shift, float* out,
+                        int B, int C, int D, int H, int W, void* stream);
+int fsmi_disparity_transformer(const float* x, float* out, const float* params, const float* pe, int B, int C,
+                               int L, int HW, int nheads, int ffdim, int nlayers, float eps, void* stream);
+int fsmi_upsample4_add(const float* t, float* vol, int B, int C, int D, int H, int W, void* stream);
+
 /* ---- live kernel timing (bench.py roofline) -----------------------------
  * When enabled, every launch of the kernels below is bracketed by a pair of
  * hipEvents recorded on the launch stream (skipped while the stream is being
@@ -237,7 +259,7 @@ int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int W
 enum {
   FSMI_K_GWC = 0, FSMI_K_CONCAT, FSMI_K_COMB, FSMI_K_PROJ, FSMI_K_CORR, FSMI_K_VOLPYR,
   FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
-  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_DWCONV, FSMI_K_RESIZE, FSMI_K_COUNT
+  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_DWCONV, FSMI_K_RESIZE, FSMI_K_DT, FSMI_K_COUNT
 };
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
