@@ -1,0 +1,48 @@
+"""Checkpoint + config loading of ``scripts/run_demo.py:111-125``.
+
+The reference reads ``cfg.yaml`` next to the checkpoint with OmegaConf, defaults
+``vit_size`` to ``vitl``, overlays the command-line args, builds
+``FoundationStereo(args)`` and loads ``torch.load(ckpt)['model']``.  OmegaConf is
+absent from this image: ``cfg.yaml`` is plain YAML, read with ``yaml.safe_load``
+into a ``StereoArgs`` (attribute, item and ``.get`` access, as OmegaConf gives).
+The checkpoint is read with ``weights_only=True``: tensors and plain containers
+only, nothing in the file is executed.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+import torch
+import yaml
+
+from .synth import StereoArgs
+
+
+def load_cfg(ckpt_path: str, overrides: Optional[dict] = None) -> StereoArgs:
+    """``cfg.yaml`` beside ``ckpt_path`` (scripts/run_demo.py:112-117)."""
+    cfg_path = os.path.join(os.path.dirname(os.path.abspath(ckpt_path)), "cfg.yaml")
+    with open(cfg_path) as f:
+        cfg = yaml.safe_load(f) or {}
+    if not isinstance(cfg, dict):
+        raise ValueError(f"{cfg_path}: expected a mapping, got {type(cfg).__name__}")
+    cfg.setdefault("vit_size", "vitl")
+    cfg.update(overrides or {})
+    return StereoArgs(cfg)
+
+
+def load_model(ckpt_path: str, overrides: Optional[dict] = None, device=None,
+               feature=None) -> Tuple[torch.nn.Module, dict]:
+    """FoundationStereo with the checkpoint's ``model`` state loaded strictly, in eval mode
+    (scripts/run_demo.py:121-129).  Returns (model, {"global_step", "epoch"} of the checkpoint)."""
+    from .foundation_stereo import FoundationStereo
+    args = load_cfg(ckpt_path, overrides)
+    model = FoundationStereo(args, feature=feature)
+    ckpt = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+    if not isinstance(ckpt, dict) or "model" not in ckpt:
+        raise KeyError(f"{ckpt_path}: no 'model' state in the checkpoint")
+    model.load_state_dict(ckpt["model"])
+    model.eval()
+    if device is not None:
+        model.to(device)
+    return model, {k: ckpt.get(k) for k in ("global_step", "epoch")}

@@ -1,0 +1,55 @@
+"""Checkpoint / cfg loading (scripts/run_demo.py:111-125) on the CPU: a checkpoint written in the
+reference's layout ({'model': state_dict, 'global_step', 'epoch'} + cfg.yaml beside it) loads
+strictly into a fresh model; a missing key or a wrong vit_size fails loudly."""
+import os
+
+import pytest
+import torch
+import yaml
+
+from foundationstereo_amd import synth
+from foundationstereo_amd.checkpoint import load_cfg, load_model
+
+
+def _write(tmp_path, vit="vits", cfg_extra=None, drop=None):
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    args = synth.make_args(max_disp=64, corr_levels=2, vit_size=vit)
+    m = FoundationStereo(args)
+    synth.init_module_(m, seed=7)
+    sd = m.state_dict()
+    if drop:
+        sd = {k: v for k, v in sd.items() if k != drop}
+    path = os.path.join(tmp_path, "model_best_bp2.pth")
+    torch.save({"model": sd, "global_step": 123, "epoch": 4}, path)
+    cfg = dict(args)
+    cfg.update(cfg_extra or {})
+    with open(os.path.join(tmp_path, "cfg.yaml"), "w") as f:
+        yaml.safe_dump(cfg, f)
+    return path, m
+
+
+def test_load_model_roundtrip(tmp_path):
+    path, ref = _write(tmp_path)
+    model, meta = load_model(path, overrides={"valid_iters": 8})
+    assert meta == {"global_step": 123, "epoch": 4}
+    assert not model.training and model.args.valid_iters == 8 and model.args.get("vit_size") == "vits"
+    a, b = model.state_dict(), ref.state_dict()
+    assert list(a) == list(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_cfg_defaults_vit_size_to_vitl(tmp_path):
+    path, _ = _write(tmp_path)
+    cfg = {k: v for k, v in synth.make_args(max_disp=64, corr_levels=2).items() if k != "vit_size"}
+    with open(os.path.join(tmp_path, "cfg.yaml"), "w") as f:
+        yaml.safe_dump(cfg, f)
+    assert load_cfg(path)["vit_size"] == "vitl"
+    with pytest.raises(RuntimeError):          # a ViT-S checkpoint does not fit the ViT-L tree
+        load_model(path)
+
+
+def test_missing_key_is_an_error(tmp_path):
+    path, ref = _write(tmp_path, drop="classifier.2.weight")
+    with pytest.raises(RuntimeError, match="classifier"):
+        load_model(path)
