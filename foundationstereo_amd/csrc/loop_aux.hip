@@ -56,6 +56,55 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
   }
 }
 
+// Single-input-channel KSxKS conv (+ bias, optional ReLU): the motion encoder's convd1,
+// Conv2d(1, 64, 7, padding=3) + ReLU (core/update.py:57,67).  Block = 16x64 output pixels x
+// CO_PER output channels (blockIdx.y); the thread's (4 + KS - 1) x KS input window is read from
+// LDS into registers once and reused for every output channel; weights are block-uniform.
+constexpr int C1_CO = 8;
+template <int KS>
+__global__ __launch_bounds__(256) void conv_1in_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ out,
+                                                       int Cout, int H, int W, int ntr, int ntc, int relu) {
+  constexpr int P = KS / 2, IR = DW_TR + KS - 1, IC = DW_TC + KS - 1;
+  __shared__ float tile[IR][IC + 1];
+  const int b = blockIdx.x / (ntr * ntc);
+  const int t = blockIdx.x - b * ntr * ntc;
+  const int r0 = (t / ntc) * DW_TR, c0 = (t % ntc) * DW_TC;
+  const float* xp = x + static_cast<size_t>(b) * H * W;
+  for (int e = threadIdx.x; e < IR * IC; e += 256) {
+    const int ir = e / IC, ic = e - ir * IC;
+    const int hh = r0 + ir - P, ww = c0 + ic - P;
+    tile[ir][ic] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xp[hh * W + ww] : 0.f;
+  }
+  __syncthreads();
+  const int col = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
+  float v[4 + KS - 1][KS];
+#pragma unroll
+  for (int ir = 0; ir < 4 + KS - 1; ++ir)
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw) v[ir][kw] = tile[rb + ir][col + kw];
+  const int co_end = min(Cout, static_cast<int>(blockIdx.y + 1) * C1_CO);
+  for (int co = blockIdx.y * C1_CO; co < co_end; ++co) {
+    const float* wk = w + co * KS * KS;                 // uniform: scalar loads
+    const float b0 = bias ? bias[co] : 0.f;
+    float acc[4] = {b0, b0, b0, b0};
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+        const float wv = wk[kh * KS + kw];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) acc[o] = fmaf(wv, v[o + kh][kw], acc[o]);
+      }
+    float* op = out + (static_cast<size_t>(b) * Cout + co) * H * W;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int hh = r0 + rb + o, ww = c0 + col;
+      if (hh < H && ww < W) op[hh * W + ww] = relu ? fmaxf(acc[o], 0.f) : acc[o];
+    }
+  }
+}
+
 // F.interpolate(mode="bilinear", align_corners=True): src = dst * (in-1)/(out-1)
 __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x, float* __restrict__ out,
                                                      long long planes, int Hi, int Wi, int Ho, int Wo, float sh,
@@ -96,6 +145,21 @@ extern "C" int fsmi_dwconv2d(const float* x, const float* w, const float* bias, 
   else if (KS == 5) hipLaunchKernelGGL(dwconv_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
   else hipLaunchKernelGGL(dwconv_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
   return finish_launch("fsmi_dwconv2d");
+}
+
+extern "C" int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,
+                               int H, int W, int relu, void* stream) {
+  FSMI_CHECK_ARG(x && w && out, "fsmi_conv2d_1in: null pointer");
+  FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "fsmi_conv2d_1in: bad shape");
+  FSMI_CHECK_ARG(KS == 3 || KS == 5 || KS == 7, "fsmi_conv2d_1in: kernel %d unsupported (3, 5, 7)", KS);
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_DWCONV, s);
+  const int ntr = (H + DW_TR - 1) / DW_TR, ntc = (W + DW_TC - 1) / DW_TC;
+  const dim3 grid(static_cast<unsigned>(B) * ntr * ntc, (Cout + C1_CO - 1) / C1_CO);
+  if (KS == 7) hipLaunchKernelGGL(conv_1in_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
+  else if (KS == 5) hipLaunchKernelGGL(conv_1in_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
+  else hipLaunchKernelGGL(conv_1in_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
+  return finish_launch("fsmi_conv2d_1in");
 }
 
 extern "C" int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo,

@@ -510,6 +510,19 @@ def dwconv2d(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
+def conv2d_1in(x: Tensor, w: Tensor, bias: Tensor = None, relu: bool = False) -> Tensor:
+    """``Conv2d(1, Cout, KS, padding=KS//2)`` (+ ReLU) -- the motion encoder's convd1."""
+    _check("conv2d_1in", x, w, *([bias] if bias is not None else []))
+    B, C, H, W = x.shape
+    Cout, KS = w.shape[0], w.shape[-1]
+    assert C == 1 and tuple(w.shape) == (Cout, 1, KS, KS), f"conv2d_1in: {tuple(x.shape)} x {tuple(w.shape)}"
+    x, w = _c(x), _c(w)
+    out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_conv2d_1in(_p(x), _p(w), _p(_c(bias)) if bias is not None else None, _p(out), B,
+                                           Cout, KS, H, W, 1 if relu else 0, _stream(x)), "conv2d_1in")
+    return out
+
+
 def resize_bilinear(x: Tensor, size) -> Tensor:
     """``F.interpolate(x, size, mode="bilinear", align_corners=True)``."""
     _check("resize_bilinear", x)

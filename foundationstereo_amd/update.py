@@ -36,6 +36,9 @@ PIPELINE = os.environ.get("FSMI_PIPELINE", "1") != "0"
 PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 
 
+_CONVD1_MIOPEN = os.environ.get("FSMI_CONVD1_MIOPEN", "0") == "1"
+
+
 def _fast(x) -> bool:
     return (CONV_ENGINE == "fsmi" and x.is_cuda and x.dtype == torch.float32
             and not torch.is_autocast_enabled() and not torch.is_grad_enabled())
@@ -146,7 +149,10 @@ class BasicMotionEncoder(nn.Module):
     def encode_into(self, disp, corr, out):
         """Writes cat([relu(conv(...)), disp]) into ``out`` (B, 128, H, W) without the cat copy."""
         c = _conv(self.convc2, [_conv(self.convc1, [corr], "relu")], "relu")
-        d = F.relu_(self.convd1(disp))                          # 7x7, 1 -> 64 (MIOpen)
+        if _CONVD1_MIOPEN:                                     # A/B knob: the MIOpen conv + ReLU
+            d = F.relu_(self.convd1(disp))
+        else:
+            d = ops.conv2d_1in(disp, self.convd1.weight, self.convd1.bias, relu=True)   # 7x7, 1 -> 64
         d = _conv(self.convd2, [d], "relu")
         _conv(self.conv, [c, d], "relu", out=out, co0=0)
         out[:, self.conv.out_channels:].copy_(disp)

@@ -228,6 +228,10 @@ int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wl
 int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
                   int H, int W, void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
+/* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
+ *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */
+int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,
+                    int H, int W, int relu, void* stream);
 
 /* ---- disparity transformer of the hourglass ---------
  * fsmi_dt_patch_embed: conv_patch = depthwise Conv3d(C, C, 4, stride 4) + eval

@@ -288,6 +288,20 @@ def test_dwconv2d_vs_torch(ops_mod, KS, shape):
     close(ops_mod.dwconv2d(g(x), g(w), g(b)), ref, atol=1e-5)
 
 
+@pytest.mark.parametrize("KS,B,cout,HW,relu", [(7, 1, 64, (120, 160), True), (7, 2, 13, (19, 70), False),
+                                              (3, 1, 9, (17, 9), True), (5, 1, 8, (33, 65), False)])
+def test_conv2d_1in_vs_torch(ops_mod, KS, B, cout, HW, relu):
+    """Single-input-channel conv (+ReLU) -- the motion encoder's convd1 -- vs the fp64 torch conv;
+    ragged pixel tiles and output-channel groups, 1e-5 abs (49-term fp32 sums)."""
+    x = synth.normal(204, (B, 1) + HW, 10.0)            # disparity-like magnitudes
+    w = synth.normal(205, (cout, 1, KS, KS), 0.2)
+    b = synth.normal(206, (cout,), 0.1)
+    ref = torch.nn.functional.conv2d(t(x).double(), t(w).double(), t(b).double(), padding=KS // 2)
+    if relu:
+        ref = ref.clamp_min(0)
+    close(ops_mod.conv2d_1in(g(x), g(w), g(b), relu=relu), ref, atol=2e-5 * 10)
+
+
 @pytest.mark.parametrize("src,dst", [((30, 40), (60, 80)), ((60, 80), (120, 160)), ((7, 5), (13, 11)),
                                      ((1, 6), (3, 6))])
 def test_resize_bilinear_vs_torch(ops_mod, src, dst):
