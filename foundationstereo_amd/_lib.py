@@ -57,6 +57,8 @@ SIGNATURES = {
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
+    "fsmi_timer_query_clock": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
+    "fsmi_timer_replay": [_I, _I, ctypes.POINTER(ctypes.c_double)],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",

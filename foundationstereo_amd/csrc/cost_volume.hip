@@ -297,11 +297,13 @@ __global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __res
                                                               const float* __restrict__ Bm,
                                                               const float* __restrict__ Wg,
                                                               float* __restrict__ out, int C, int Cs, int D,
-                                                              int H, int W, int WQ, int DQN, int nwt, int ndc, int dbg) {
+                                                              int H, int W, int WQ, int DQN, int nwt, int ndc, int dbg,
+                                                              unsigned long long* clk) {
   constexpr int G = kBuildG, NPH = G / GP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Cg = C / G;
   const int WT = 4 * WQ, DCH = 4 * DQN, RS = WT + DCH, NC = WT + RS;
+  clock_begin(clk);
   const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
   const int dc = item % ndc;
   const int rest = item / ndc;
@@ -497,6 +499,7 @@ __global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __res
     __builtin_amdgcn_s_waitcnt(0);
     ts[11] = wall_clock64();
   }
+  clock_end(clk);
 }
 
 // a2: out (B,2C,D,H,W); one thread per output element, w fastest.
@@ -628,14 +631,19 @@ int launch_build_stem(const float* fl, const float* fr, const float* A, const fl
   const char* dbs = std::getenv("FSMI_BUILD_DBG");
   const int dbg = dbs ? std::atoi(dbs) : 0;
   LaunchTimer t(FSMI_K_COMB, s);
+  unsigned long long* clk = clock_slot(FSMI_K_COMB, s, static_cast<long long>(grid) * (nthr / kWave));
 #define FSMI_BUILD_CASE(V, P)                                                                                     \
   do {                                                                                                            \
     const void* fn = reinterpret_cast<const void*>(build_stem_kernel<V, P>);                                      \
     if (lds > 64 * 1024 &&                                                                                        \
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess) \
       return finish_launch("fsmi_comb_volume_stem: LDS attribute");                                               \
+    set_replay(FSMI_K_COMB, s, [=] {                                                                              \
+      hipLaunchKernelGGL((build_stem_kernel<V, P>), dim3(grid), dim3(nthr), lds, s, fl, fr, A, Bm, Wg, out, C, Cs,  \
+                         D, H, W, WQ, DQN, nwt, ndc, dbg, nullptr);                                               \
+    });                                                                                                           \
     hipLaunchKernelGGL((build_stem_kernel<V, P>), dim3(grid), dim3(nthr), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D, \
-                       H, W, WQ, DQN, nwt, ndc, dbg);                                                             \
+                       H, W, WQ, DQN, nwt, ndc, dbg, clk);                                                        \
   } while (0)
   if (vec) {
     if (GP == 8) FSMI_BUILD_CASE(4, 8);

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <functional>
 #include <string>
 
 #include "../../include/fsmi.h"
@@ -32,6 +33,36 @@ class LaunchTimer {
 };
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// In-kernel launch clock (runtime.hip): while timing is on and the stream is not being captured,
+// an instrumented launch gets a zeroed device array of 2 x nwaves stamps (s_memrealtime, 100 MHz):
+// every wave stores its start at the top and its end after its stores are acknowledged -- plain
+// stores to its own slot, no atomics (same-address atomics from ~10k waves cost the lookup 3x).
+// The host takes max(end) - min(start) per launch; waves that exit early leave a 0 end.
+// nullptr otherwise (graph replays carry no clock).  bench.py divides the roofline bytes by this
+// duration: the kernel's execution time, without the event-record latency around a launch.
+unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves);
+
+// Replay hook for fsmi_timer_replay: while timing is on (and not capturing), an instrumented
+// entry point registers a closure that re-issues its last launch with identical arguments on the
+// same stream (the kernels are pure functions of their inputs, so re-running them rewrites the
+// same outputs).  bench.py times a back-to-back batch of replays between two hipEvents, which
+// amortises the event-record latency a single bracketed launch carries.
+void set_replay(int kernel, hipStream_t stream, std::function<void()> fn);
+
+__device__ __forceinline__ long long clock_wave_id() {
+  const long long blk = blockIdx.x + static_cast<long long>(gridDim.x) * (blockIdx.y + static_cast<long long>(gridDim.y) * blockIdx.z);
+  return blk * ((blockDim.x * blockDim.y * blockDim.z + 63) / 64) + (threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z)) / 64;
+}
+__device__ __forceinline__ void clock_begin(unsigned long long* slot) {
+  if (slot && (threadIdx.x & 63) == 0) slot[2 * clock_wave_id()] = wall_clock64();
+}
+__device__ __forceinline__ void clock_end(unsigned long long* slot) {
+  if (slot) {
+    __builtin_amdgcn_s_waitcnt(0);
+    if ((threadIdx.x & 63) == 0) slot[2 * clock_wave_id() + 1] = wall_clock64();
+  }
+}
 
 inline int finish_launch(const char* what) {
   hipError_t e = hipGetLastError();

@@ -256,6 +256,7 @@ struct LookupArgs {
   const float* disp;
   float* out;
   int L, Cv, D, H, W, W2, B;
+  unsigned long long* clk;   // in-kernel launch clock (nullptr: off)
 };
 
 // FP contraction is OFF for the coordinate math: fusing `ix - floor(ix)` into
@@ -321,6 +322,7 @@ __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
   constexpr int K = 2 * R + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = blockIdx.y;  // level
+  clock_begin(a.clk);
   const int chunk = blockIdx.z * 4 + wave;
   const int nchunk_geo = (a.Cv + kCPC - 1) / kCPC;
   if (chunk > nchunk_geo) return;
@@ -356,6 +358,7 @@ __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
     tp.init(static_cast<float>(w) / s - ds, W2i);
     tp.sample(row, 1, W2i, outp + static_cast<size_t>(base + a.Cv * K) * HW, HW);
   }
+  clock_end(a.clk);
 }
 
 // bilinear_sampler 1-D: img (P,C,1,Lx), x (P,K) -> out (P,C,1,K)
@@ -463,11 +466,17 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
   dim3 grid(ceil_div(P, 64), num_levels, (nchunk + 3) / 4);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_LOOKUP, s);
-  switch (radius) {
-    case 2: hipLaunchKernelGGL(geo_lookup_kernel<2>, grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(geo_lookup_kernel<3>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(geo_lookup_kernel<4>, grid, dim3(256), 0, s, a); break;
-  }
+  auto launch = [grid, radius, s](const LookupArgs& la) {
+    switch (radius) {
+      case 2: hipLaunchKernelGGL(geo_lookup_kernel<2>, grid, dim3(256), 0, s, la); break;
+      case 3: hipLaunchKernelGGL(geo_lookup_kernel<3>, grid, dim3(256), 0, s, la); break;
+      default: hipLaunchKernelGGL(geo_lookup_kernel<4>, grid, dim3(256), 0, s, la); break;
+    }
+  };
+  a.clk = nullptr;
+  set_replay(FSMI_K_LOOKUP, s, [launch, a] { launch(a); });
+  a.clk = clock_slot(FSMI_K_LOOKUP, s, static_cast<long long>(grid.x) * grid.y * grid.z * 4);
+  launch(a);
   return finish_launch("fsmi_geo_lookup");
 }
 

@@ -48,6 +48,49 @@ bool take(int k, hipEvent_t* s, hipEvent_t* e) {
 }
 }  // namespace
 
+// in-kernel clock: a device arena of per-wave (start, end) stamps, bump-allocated per launch and
+// zeroed at enable / reset; per kernel the host keeps (offset, nwaves) of each launch
+constexpr size_t kClockArena = size_t(1) << 22;       // u64 stamps (32 MB)
+unsigned long long* g_clock = nullptr;
+size_t g_clock_top = 0;
+std::vector<std::pair<size_t, long long>> g_clock_launch[FSMI_K_COUNT];
+
+static int clock_init() {
+  if (!g_clock && hipMalloc(&g_clock, sizeof(unsigned long long) * kClockArena) != hipSuccess) {
+    g_clock = nullptr;
+    return FSMI_ERR_ARG;
+  }
+  if (hipMemset(g_clock, 0, sizeof(unsigned long long) * kClockArena) != hipSuccess) return FSMI_ERR_ARG;
+  g_clock_top = 0;
+  for (auto& v : g_clock_launch) v.clear();
+  return FSMI_OK;
+}
+
+unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves) {
+  if (!g_enabled || !g_clock || nwaves <= 0) return nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  const size_t need = 2 * static_cast<size_t>(nwaves);
+  if (g_clock_top + need > kClockArena) return nullptr;
+  g_clock_launch[kernel].emplace_back(g_clock_top, nwaves);
+  unsigned long long* p = g_clock + g_clock_top;
+  g_clock_top += need;
+  return p;
+}
+
+std::function<void()> g_replay[FSMI_K_COUNT];
+hipStream_t g_replay_stream[FSMI_K_COUNT];
+
+void set_replay(int kernel, hipStream_t stream, std::function<void()> fn) {
+  if (!g_enabled) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_replay[kernel] = std::move(fn);
+  g_replay_stream[kernel] = stream;
+}
+
 LaunchTimer::LaunchTimer(int kernel, hipStream_t stream) : stream_(stream) {
   if (!g_enabled) return;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -77,6 +120,10 @@ int fsmi_timer_enable(int on) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   fsmi::g_enabled = on != 0;
   if (fsmi::g_enabled) {
+    if (fsmi::clock_init() != FSMI_OK) {
+      fsmi::set_error("fsmi_timer_enable: clock slots");
+      return FSMI_ERR_ARG;
+    }
     for (auto& p : fsmi::g_pool) {  // pre-create so the timed region does not pay for it
       while (p.start.size() < 64) {
         hipEvent_t a, b;
@@ -95,6 +142,80 @@ int fsmi_timer_enable(int on) {
 int fsmi_timer_reset(void) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   for (auto& p : fsmi::g_pool) p.used = 0;
+  if (fsmi::g_enabled) {
+    if (hipDeviceSynchronize() != hipSuccess || fsmi::clock_init() != FSMI_OK) {
+      fsmi::set_error("fsmi_timer_reset: clock slots");
+      return FSMI_ERR_ARG;
+    }
+  }
+  return FSMI_OK;
+}
+
+int fsmi_timer_replay(int kernel, int reps, double* avg_ms) {
+  FSMI_CHECK_ARG(kernel >= 0 && kernel < FSMI_K_COUNT && reps > 0, "fsmi_timer_replay: kernel %d reps %d", kernel,
+                 reps);
+  std::function<void()> fn;
+  hipStream_t s;
+  {
+    std::lock_guard<std::mutex> lk(fsmi::g_mu);
+    fn = fsmi::g_replay[kernel];
+    s = fsmi::g_replay_stream[kernel];
+  }
+  FSMI_CHECK_ARG(static_cast<bool>(fn), "fsmi_timer_replay: no recorded launch of kernel %d", kernel);
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+    fsmi::set_error("fsmi_timer_replay: hipEventCreate failed");
+    return FSMI_ERR_ARG;
+  }
+  hipError_t e = hipStreamSynchronize(s);
+  fn();                                          // one untimed replay
+  if (e == hipSuccess) e = hipEventRecord(e0, s);
+  for (int i = 0; i < reps && e == hipSuccess; ++i) fn();
+  if (e == hipSuccess) e = hipEventRecord(e1, s);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (e != hipSuccess) {
+    fsmi::set_error("fsmi_timer_replay: %s", hipGetErrorString(e));
+    return static_cast<int>(e);
+  }
+  if (avg_ms) *avg_ms = static_cast<double>(ms) / reps;
+  return FSMI_OK;
+}
+
+int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count) {
+  FSMI_CHECK_ARG(kernel >= 0 && kernel < FSMI_K_COUNT, "fsmi_timer_query_clock: bad kernel id %d", kernel);
+  std::lock_guard<std::mutex> lk(fsmi::g_mu);
+  const auto& launches = fsmi::g_clock_launch[kernel];
+  double tot = 0.0;
+  long long n = 0;
+  if (!launches.empty()) {
+    hipError_t e = hipDeviceSynchronize();
+    std::vector<unsigned long long> v;
+    for (const auto& l : launches) {
+      v.resize(2 * static_cast<size_t>(l.second));
+      if (e == hipSuccess)
+        e = hipMemcpy(v.data(), fsmi::g_clock + l.first, v.size() * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        fsmi::set_error("fsmi_timer_query_clock: %s", hipGetErrorString(e));
+        return static_cast<int>(e);
+      }
+      unsigned long long t0 = ~0ULL, t1 = 0;
+      for (size_t i = 0; i < v.size(); i += 2) {
+        if (v[i]) t0 = std::min(t0, v[i]);
+        t1 = std::max(t1, v[i + 1]);
+      }
+      if (t1 > t0) {
+        tot += static_cast<double>(t1 - t0) * 1e-5;   // 100 MHz ticks -> ms
+        ++n;
+      }
+    }
+  }
+  if (total_ms) *total_ms = tot;
+  if (count) *count = n;
   return FSMI_OK;
 }
 

@@ -621,6 +621,27 @@ def conv_flops() -> int:
     return _CONV_FLOPS["flops"]
 
 
+def timer_replay(kernel: str, reps: int = 20) -> float:
+    """Average ms of ``reps`` back-to-back replays of the last timed launch of ``kernel``
+    (lookup / comb), between two hipEvents on its stream."""
+    import ctypes
+    ms = ctypes.c_double(0.0)
+    _lib.check(_lib.load().fsmi_timer_replay(_lib.KERNELS.index(kernel), int(reps), ctypes.byref(ms)),
+               "timer_replay")
+    return ms.value
+
+
+def timer_query_clock(kernel: str):
+    """(total_ms, launches) of ``kernel`` since the last reset from the kernel's own clock
+    (first block start to last wave end); lookup and cost-volume build only."""
+    import ctypes
+    tot = ctypes.c_double(0.0)
+    cnt = ctypes.c_longlong(0)
+    _lib.check(_lib.load().fsmi_timer_query_clock(_lib.KERNELS.index(kernel), ctypes.byref(tot),
+                                                  ctypes.byref(cnt)), "timer_query_clock")
+    return tot.value, cnt.value
+
+
 def timer_query(kernel: str):
     """(total_ms, launches) of ``kernel`` since the last reset (synchronises its events)."""
     import ctypes

@@ -268,6 +268,15 @@ enum {
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
 int fsmi_timer_query(int kernel, double* total_ms, long long* count);
+/* Same launches timed by the kernels themselves (lookup and cost-volume build only): each
+ * instrumented launch records its first block start and last wave end (stores acknowledged) in
+ * s_memrealtime ticks; returns the summed durations -- execution time without the latency of
+ * the event records around the launch. */
+int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count);
+/* Re-issue the last timed launch of `kernel` (lookup, cost-volume build) `reps` times back to
+ * back on its stream between two hipEvents; *avg_ms = span / reps.  The kernels are pure
+ * functions of their inputs, so the replays rewrite identical outputs. */
+int fsmi_timer_replay(int kernel, int reps, double* avg_ms);
 
 #ifdef __cplusplus
 }

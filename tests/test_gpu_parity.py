@@ -537,3 +537,25 @@ def test_hierarchical_runs(ops_mod):
     with torch.no_grad():
         out = m.run_hierachical(g(left), g(right), iters=2, test_mode=True)
     assert out.shape == (1, 1, 200, 300) and torch.isfinite(out).all()
+
+
+def test_timer_clock_and_replay(ops_mod):
+    """bench.py's roofline timing hooks: with timing on, a build launch records an in-kernel clock
+    span and a replay closure; replays rewrite identical outputs and report a positive duration."""
+    gen = torch.Generator().manual_seed(5)
+    C, Cs, H, W, D = 64, 28, 6, 40, 12
+    fl, fr = (torch.randn(1, C, H, W, generator=gen).to(DEV) for _ in range(2))
+    A, Bm = (torch.randn(1, Cs, H, W, generator=gen).to(DEV) for _ in range(2))
+    Wg = (torch.randn(Cs, 8, generator=gen) * 0.3).to(DEV)
+    ops_mod.timer_enable(True)
+    try:
+        ops_mod.timer_reset()
+        out = ops_mod.comb_volume_stem(fl, fr, A, Bm, Wg, D)
+        ref = out.clone()
+        ms, n = ops_mod.timer_query_clock("comb")
+        assert n == 1 and ms > 0
+        avg = ops_mod.timer_replay("comb", 3)
+        torch.cuda.synchronize()
+        assert avg > 0 and torch.equal(out, ref)
+    finally:
+        ops_mod.timer_enable(False)
