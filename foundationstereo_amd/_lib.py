@@ -48,6 +48,7 @@ SIGNATURES = {
                             ctypes.c_longlong, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_pool2x": [_P, _P, _I, _I, _I, _I, _P],
     "fsmi_conv2d_1in": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_dt_layer_floats": [],
     "fsmi_dt_patch_embed": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],

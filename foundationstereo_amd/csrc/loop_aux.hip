@@ -105,6 +105,30 @@ __global__ __launch_bounds__(256) void conv_1in_kernel(const float* __restrict__
   }
 }
 
+// pool2x: F.avg_pool2d(x, 3, stride=2, padding=1) with count_include_pad (every window / 9),
+// core/update.py:72-73.  One thread per output; the 3 input rows are contiguous 3-float runs.
+__global__ __launch_bounds__(256) void pool2x_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                     int H, int W, int Ho, int Wo, long long n) {
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int ox = static_cast<int>(i % Wo);
+  const int oy = static_cast<int>((i / Wo) % Ho);
+  const long long p = i / (static_cast<long long>(Ho) * Wo);
+  const float* xp = x + p * H * W;
+  float s = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int y = 2 * oy + dy;
+    if (y < 0 || y >= H) continue;
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int xx = 2 * ox + dx;
+      if (xx >= 0 && xx < W) s += xp[y * W + xx];
+    }
+  }
+  out[i] = s / 9.f;
+}
+
 // F.interpolate(mode="bilinear", align_corners=True): src = dst * (in-1)/(out-1)
 __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x, float* __restrict__ out,
                                                      long long planes, int Hi, int Wi, int Ho, int Wo, float sh,
@@ -160,6 +184,17 @@ extern "C" int fsmi_conv2d_1in(const float* x, const float* w, const float* bias
   else if (KS == 5) hipLaunchKernelGGL(conv_1in_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
   else hipLaunchKernelGGL(conv_1in_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
   return finish_launch("fsmi_conv2d_1in");
+}
+
+extern "C" int fsmi_pool2x(const float* x, float* out, int B, int C, int H, int W, void* stream) {
+  FSMI_CHECK_ARG(x && out, "fsmi_pool2x: null pointer");
+  FSMI_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0, "fsmi_pool2x: bad shape");
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_RESIZE, s);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long n = static_cast<long long>(B) * C * Ho * Wo;
+  hipLaunchKernelGGL(pool2x_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, x, out, H, W, Ho, Wo, n);
+  return finish_launch("fsmi_pool2x");
 }
 
 extern "C" int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo,

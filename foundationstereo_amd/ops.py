@@ -510,6 +510,16 @@ def dwconv2d(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
+def pool2x(x: Tensor) -> Tensor:
+    """``F.avg_pool2d(x, 3, stride=2, padding=1)`` (count_include_pad: every window / 9)."""
+    _check("pool2x", x)
+    B, C, H, W = x.shape
+    x = _c(x)
+    out = torch.empty((B, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_pool2x(_p(x), _p(out), B, C, H, W, _stream(x)), "pool2x")
+    return out
+
+
 def conv2d_1in(x: Tensor, w: Tensor, bias: Tensor = None, relu: bool = False) -> Tensor:
     """``Conv2d(1, Cout, KS, padding=KS//2)`` (+ ReLU) -- the motion encoder's convd1."""
     _check("conv2d_1in", x, w, *([bias] if bias is not None else []))

@@ -37,6 +37,7 @@ PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 
 
 _CONVD1_MIOPEN = os.environ.get("FSMI_CONVD1_MIOPEN", "0") == "1"
+_POOL_TORCH = os.environ.get("FSMI_POOL_TORCH", "0") == "1"        # A/B knob: torch avg_pool2d
 
 
 def _fast(x) -> bool:
@@ -169,6 +170,8 @@ class BasicMotionEncoder(nn.Module):
 
 
 def pool2x(x):
+    if _fast(x) and not _POOL_TORCH:
+        return ops.pool2x(x)
     return F.avg_pool2d(x, 3, stride=2, padding=1)
 
 

@@ -230,6 +230,9 @@ int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out,
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
  *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */
+/* fsmi_pool2x: F.avg_pool2d(x, 3, stride=2, padding=1) (count_include_pad) on (B,C,H,W) ->
+ *   (B,C,(H-1)/2+1,(W-1)/2+1): pool2x, core/update.py:72-73. */
+int fsmi_pool2x(const float* x, float* out, int B, int C, int H, int W, void* stream);
 int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,
                     int H, int W, int relu, void* stream);
 

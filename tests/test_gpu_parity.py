@@ -288,6 +288,14 @@ def test_dwconv2d_vs_torch(ops_mod, KS, shape):
     close(ops_mod.dwconv2d(g(x), g(w), g(b)), ref, atol=1e-5)
 
 
+@pytest.mark.parametrize("shape", [(1, 128, 60, 80), (2, 3, 7, 9), (1, 2, 1, 1), (1, 4, 30, 40)])
+def test_pool2x_vs_torch(ops_mod, shape):
+    """pool2x (avg 3x3, stride 2, pad 1, count_include_pad) vs the torch CPU fp32 op."""
+    x = synth.normal(207, shape)
+    ref = torch.nn.functional.avg_pool2d(t(x), 3, stride=2, padding=1)
+    close(ops_mod.pool2x(g(x)), ref, atol=2e-6)
+
+
 @pytest.mark.parametrize("KS,B,cout,HW,relu", [(7, 1, 64, (120, 160), True), (7, 2, 13, (19, 70), False),
                                               (3, 1, 9, (17, 9), True), (5, 1, 8, (33, 65), False)])
 def test_conv2d_1in_vs_torch(ops_mod, KS, B, cout, HW, relu):
