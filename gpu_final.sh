@@ -3,4 +3,4 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1
-bash tools/gpu_round_profile.sh > gpurun_out/round_profile.log 2>&1
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err
