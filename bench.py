@@ -242,7 +242,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f16-conv/f32-volume" if a.mixed_precision else "f32",
+        # fp32 arithmetic throughout; the convs run as 3 fp16 MFMA products per MAC on fp16 hi/lo
+        # splits (~22-bit operand mantissas, fp32 accumulation), not as fp32 MFMA
+        "dtype": ("f32 (3xfp16 split MFMA convs; library convs fp16 under autocast)" if a.mixed_precision
+                  else "f32 (3xfp16 split MFMA)"),
         "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
         "config": {"workload": f"{a.config}: {W}x{H}, max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",

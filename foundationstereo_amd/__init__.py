@@ -29,8 +29,15 @@ def patch_reference(core_foundation_stereo_module):
     globals makes an unmodified reference ``FoundationStereo`` build and run
     this package's modules.  Returns the list of names replaced.
     """
-    from . import geometry, submodule, update, utils
+    from . import extractor, foundation_stereo, geometry, submodule, update, utils
     replaced = []
+    # ContextNetDino (core/extractor.py, star-imported at :17) and hourglass (defined in
+    # core/foundation_stereo.py:45-123 itself) carry the halo-kernel / disparity-transformer fast
+    # paths; their module trees, hence state_dict keys, are the reference's
+    for name, obj in (("ContextNetDino", extractor.ContextNetDino), ("hourglass", foundation_stereo.hourglass)):
+        if hasattr(core_foundation_stereo_module, name):
+            setattr(core_foundation_stereo_module, name, obj)
+            replaced.append(name)
     for mod in (submodule, update, utils):
         for name in getattr(mod, "__all__", []):
             if hasattr(core_foundation_stereo_module, name):

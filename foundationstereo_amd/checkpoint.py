@@ -34,15 +34,29 @@ def load_cfg(ckpt_path: str, overrides: Optional[dict] = None) -> StereoArgs:
 def load_model(ckpt_path: str, overrides: Optional[dict] = None, device=None,
                feature=None) -> Tuple[torch.nn.Module, dict]:
     """FoundationStereo with the checkpoint's ``model`` state loaded strictly, in eval mode
-    (scripts/run_demo.py:121-129).  Returns (model, {"global_step", "epoch"} of the checkpoint)."""
+    (scripts/run_demo.py:121-129).  Returns (model, meta): meta holds the checkpoint's
+    ``global_step`` / ``epoch`` and ``skipped_backbone_keys``.
+
+    A real checkpoint carries the backbone's ``feature.*`` weights (EdgeNeXt + DepthAnythingV2,
+    out of this package's scope).  When ``feature`` is None (the parameter-free synthetic
+    stand-in) or has no parameters of its own, those keys cannot be loaded anywhere: they are
+    set aside and listed in ``meta["skipped_backbone_keys"]``, and every other key still loads
+    strictly.  With a backbone that has parameters, ``feature.*`` must match it exactly."""
     from .foundation_stereo import FoundationStereo
     args = load_cfg(ckpt_path, overrides)
     model = FoundationStereo(args, feature=feature)
     ckpt = torch.load(ckpt_path, map_location="cpu", weights_only=True)
     if not isinstance(ckpt, dict) or "model" not in ckpt:
         raise KeyError(f"{ckpt_path}: no 'model' state in the checkpoint")
-    model.load_state_dict(ckpt["model"])
+    state = ckpt["model"]
+    skipped = []
+    if not any(True for _ in model.feature.state_dict()):
+        skipped = [k for k in state if k.startswith("feature.")]
+        state = {k: v for k, v in state.items() if not k.startswith("feature.")}
+    model.load_state_dict(state)
     model.eval()
     if device is not None:
         model.to(device)
-    return model, {k: ckpt.get(k) for k in ("global_step", "epoch")}
+    meta = {k: ckpt.get(k) for k in ("global_step", "epoch")}
+    meta["skipped_backbone_keys"] = skipped
+    return model, meta

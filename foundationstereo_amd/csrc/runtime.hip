@@ -119,6 +119,7 @@ const char* fsmi_arch(void) { return "gfx950"; }
 int fsmi_timer_enable(int on) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   fsmi::g_enabled = on != 0;
+  for (auto& f : fsmi::g_replay) f = nullptr;      // a replay only targets buffers of the current session
   if (fsmi::g_enabled) {
     if (fsmi::clock_init() != FSMI_OK) {
       fsmi::set_error("fsmi_timer_enable: clock slots");
@@ -142,6 +143,7 @@ int fsmi_timer_enable(int on) {
 int fsmi_timer_reset(void) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   for (auto& p : fsmi::g_pool) p.used = 0;
+  for (auto& f : fsmi::g_replay) f = nullptr;
   if (fsmi::g_enabled) {
     if (hipDeviceSynchronize() != hipSuccess || fsmi::clock_init() != FSMI_OK) {
       fsmi::set_error("fsmi_timer_reset: clock slots");

@@ -249,8 +249,11 @@ extern "C" int fsmi_dt_patch_embed(const float* x, const float* w, const float* 
                                    int B, int C, int D, int H, int W, void* stream) {
   FSMI_CHECK_ARG(x && w && scale && shift && out, "fsmi_dt_patch_embed: null pointer");
   FSMI_CHECK_ARG(B > 0 && C > 0 && D >= 4 && H >= 4 && W >= 4, "fsmi_dt_patch_embed: bad shape");
-  FSMI_CHECK_ARG(W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0,
-                 "fsmi_dt_patch_embed: W %% 4 and a 16-B aligned input required (W=%d)", W);
+  // the kernel strides the input by 4*Do planes / 4*Ho rows: a floor (as Conv3d k4 s4 does) would
+  // need the true D / H as strides, so ragged sizes are refused instead of silently misread
+  FSMI_CHECK_ARG(D % 4 == 0 && H % 4 == 0 && W % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0,
+                 "fsmi_dt_patch_embed: D, H, W %% 4 == 0 and a 16-B aligned input required (D=%d H=%d W=%d)", D, H,
+                 W);
   hipStream_t s = as_stream(stream);
   LaunchTimer tm(FSMI_K_DT, s);
   const int Do = D / 4, Ho = H / 4, Wo = W / 4;

@@ -147,6 +147,7 @@ class SyntheticFeature(nn.Module):
         self.args = args
         self.d_out, self.vit_dim = synth.feature_dims(args.vit_size)
         self._preset = None
+        self.shift_px = 0          # right-map shift of the synthesised features (no preset)
 
     def set_features(self, left, right, vit):
         self._preset = (list(left), list(right), vit)
@@ -154,7 +155,7 @@ class SyntheticFeature(nn.Module):
     def forward(self, x):
         if self._preset is None:
             B2, _, H, W = x.shape
-            fl, fr, vit = synth.backbone_features(B2 // 2, H, W, self.args.vit_size)
+            fl, fr, vit = synth.backbone_features(B2 // 2, H, W, self.args.vit_size, shift_px=self.shift_px)
             left = [torch.from_numpy(a).to(x.device) for a in fl]
             right = [torch.from_numpy(a).to(x.device) for a in fr]
             vit = torch.from_numpy(vit).to(x.device)

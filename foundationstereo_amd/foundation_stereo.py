@@ -7,7 +7,9 @@ is the data path:
 * a1+a2: gwc + concat + the 1x1x1 ``corr_stem[0]`` conv are ONE kernel
   (``ops.comb_volume_stem``) writing the 28-channel stem volume directly --
   the 32-channel comb volume and its cat copy never exist in HBM;
-* a3: 3D filtering on MIOpen (``torch.nn``);
+* a3: 3D filtering: every stride-1 Conv3d + BN block on the halo split-precision kernel
+  (``ops.conv3d``), the classifier head on ``ops.conv3d_direct``, the disparity transformer
+  on ``ops.disparity_transformer``; strided / transposed 3D convs on MIOpen;
 * a4: softmax + soft-argmin fused (``ops.softmax_regression``); skipped when an
   ``init_disp`` is supplied (hierarchical pass) since the reference discards it;
 * a5/a6: geometry encoding + per-iteration lookup on HIP (``geometry.py``);
@@ -107,16 +109,16 @@ class hourglass(nn.Module):
         if self._dt_fast(x, conv):
             # patch embed, transformer and the x4 trilinear add on HIP (csrc/transformer.hip)
             scale, shift = self._patch_fold()
-            t = self.atts["4"](ops.dt_patch_embed(x, self.conv_patch[0].weight, scale, shift))
-            return self.conv_out(ops.upsample4_add_(conv.contiguous(), t))
+            t = self.atts["4"](ops.dt_patch_embed(_sub._f32(x), self.conv_patch[0].weight.float(), scale, shift))
+            return self.conv_out(ops.upsample4_add_(conv.float().contiguous(), t))
         t = self.atts["4"](self.conv_patch(x))
         conv = conv + F.interpolate(t, scale_factor=4, mode="trilinear", align_corners=False)
         return self.conv_out(conv)
 
     def _dt_fast(self, x, conv) -> bool:
         pc, bn = self.conv_patch[0], self.conv_patch[1]
-        return (x.is_cuda and x.dtype == torch.float32 and conv.dtype == torch.float32 and not self.training
-                and not torch.is_grad_enabled() and not torch.is_autocast_enabled() and _sub.DT_FAST
+        return (x.is_cuda and x.dtype in _sub.HIP_DTYPES and conv.dtype in _sub.HIP_DTYPES and not self.training
+                and not torch.is_grad_enabled() and _sub.DT_FAST
                 and pc.groups == pc.in_channels == pc.out_channels and pc.kernel_size == (4, 4, 4)
                 and pc.stride == (4, 4, 4) and pc.padding == (0, 0, 0) and bn.track_running_stats
                 and all(n % 4 == 0 for n in x.shape[2:]) and tuple(conv.shape) == tuple(x.shape))
@@ -250,7 +252,9 @@ class FoundationStereo(nn.Module):
         disp = init_disp.float()
         disp_preds = []
         disp_up = None
-        overlap = _update.OVERLAP and not mp and _update._fast(disp)
+        overlap = _update.OVERLAP and _update._fast(disp)
+        if overlap:     # fp32 state for the HIP loop (fp16 / bf16 context features under autocast)
+            net_list, inp_list, att = _update._f32s(net_list), _update._f32s(inp_list), _update._f32s(att)
         if overlap and test_mode and self.args.n_gru_layers == 3 and iters > 0 and _update.PIPELINE:
             # gru16 / gru08 one iteration ahead on their own stream (same math, see run_pipelined)
             net_list, mask_feat_4, disp = self.update_block.run_pipelined(net_list, inp_list, geo_fn,

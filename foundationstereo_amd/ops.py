@@ -103,6 +103,7 @@ def comb_volume_stem(fl: Tensor, fr: Tensor, A: Tensor, Bm: Tensor, Wg: Tensor, 
     _lib.check(_lib.load().fsmi_comb_volume_stem(_p(fl), _p(fr), _p(A), _p(Bm), _p(Wg),
                                                  _p(ws) if ws is not None else None, _p(out), B, C, G, Cs,
                                                  maxdisp, H, W, _stream(fl)), "comb_volume_stem")
+    _keep_for_replay("comb", fl, fr, A, Bm, Wg, ws, out)
     return out
 
 
@@ -160,6 +161,7 @@ def geo_lookup(vol_levels: Sequence[Tensor], corr_levels: Sequence[Tensor], disp
     _lib.check(_lib.load().fsmi_geo_lookup(pv, pc, _p(disp), _p(out), L, radius, B, Cv, D, H, W, W2,
                                            _stream(disp)), "geo_lookup")
     del kv, kc
+    _keep_for_replay("lookup", *vol_levels, *corr_levels, disp, out)
     return out
 
 
@@ -553,6 +555,8 @@ def dt_patch_embed(x: Tensor, w: Tensor, scale: Tensor, shift: Tensor) -> Tensor
     _check("dt_patch_embed", x, w, scale, shift)
     B, C, D, H, W = x.shape
     assert tuple(w.shape) == (C, 1, 4, 4, 4) and scale.numel() == C and shift.numel() == C
+    if D % 4 or H % 4 or W % 4:
+        raise RuntimeError(f"dt_patch_embed: D, H, W must be multiples of 4, got {(D, H, W)}")
     x, w, scale, shift = _c(x), _c(w), _c(scale), _c(shift)
     out = torch.empty((B, C, D // 4, H // 4, W // 4), device=x.device, dtype=torch.float32)
     _lib.check(_lib.load().fsmi_dt_patch_embed(_p(x), _p(w), _p(scale), _p(shift), _p(out), B, C, D, H, W,
@@ -616,15 +620,27 @@ def upsample4_add_(vol: Tensor, t: Tensor) -> Tensor:
 # timer_reset() while timers are enabled -- the numerator of bench.py's conv roofline
 _CONV_FLOPS = {"on": False, "flops": 0}
 
+# the tensors of the last timed launch per replayable kernel: fsmi_timer_replay re-issues that
+# launch with its raw pointers, so they stay allocated (not recycled by the caching allocator)
+# until the next timer_reset / timer_enable, which also drop the recorded launch on the C side
+_REPLAY_KEEP = {}
+
+
+def _keep_for_replay(kernel: str, *tensors):
+    if _CONV_FLOPS["on"] and not torch.cuda.is_current_stream_capturing():
+        _REPLAY_KEEP[kernel] = tensors
+
 
 def timer_enable(on: bool = True):
     _lib.check(_lib.load().fsmi_timer_enable(1 if on else 0), "timer_enable")
     _CONV_FLOPS["on"] = bool(on)
+    _REPLAY_KEEP.clear()
 
 
 def timer_reset():
     _lib.check(_lib.load().fsmi_timer_reset(), "timer_reset")
     _CONV_FLOPS["flops"] = 0
+    _REPLAY_KEEP.clear()
 
 
 def conv_flops() -> int:
@@ -633,7 +649,10 @@ def conv_flops() -> int:
 
 def timer_replay(kernel: str, reps: int = 20) -> float:
     """Average ms of ``reps`` back-to-back replays of the last timed launch of ``kernel``
-    (lookup / comb), between two hipEvents on its stream."""
+    (lookup / comb), between two hipEvents on its stream.  The launch's tensors are held in
+    ``_REPLAY_KEEP`` since it was recorded, so the replays write only memory they own."""
+    if kernel not in _REPLAY_KEEP:
+        raise RuntimeError(f"timer_replay: no timed launch of {kernel!r} since the last timer reset")
     import ctypes
     ms = ctypes.c_double(0.0)
     _lib.check(_lib.load().fsmi_timer_replay(_lib.KERNELS.index(kernel), int(reps), ctypes.byref(ms)),

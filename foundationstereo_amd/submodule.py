@@ -8,10 +8,12 @@ Stride-1 3D conv blocks (``BasicConv``, ``Conv3dNormActReduced``,
 ``ResnetBasicBlock3D``) and stride-1 2D ``BasicConv``s run the halo split-precision
 conv kernel with the eval BatchNorm folded into the packed weights (``conv3d_bn_act``,
 ``conv2d_bn_act``); strided / transposed convs stay on MIOpen through ``torch.nn``.
+Under autocast the HIP paths still run (inputs cast up, fp32 compute).
 
-The disparity transformer's attention uses PyTorch SDPA in place of the
-reference's third-party ``flash_attn_func`` (core/submodule.py:224): same
-non-causal softmax(QK^T/sqrt(d))V math.
+The disparity transformer runs as one HIP kernel (``ops.disparity_transformer``); its
+torch path uses PyTorch SDPA in place of the reference's third-party
+``flash_attn_func`` (core/submodule.py:224): same softmax(QK^T/sqrt(d))V math, with
+``window_size`` as a local-attention mask.
 """
 from __future__ import annotations
 
@@ -52,10 +54,21 @@ FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
 DT_FAST = os.environ.get("FSMI_DT", "1") != "0"      # disparity transformer on csrc/transformer.hip
 
 
+# Input dtypes the HIP paths accept.  Under the reference's fp16 autocast (scripts/run_demo.py:161)
+# activations arriving from library ops are fp16 / bf16: they are cast up and the HIP kernels
+# compute in fp32 (fp32 out), instead of dropping the layer to MIOpen fp16.
+HIP_DTYPES = (torch.float32, torch.float16, torch.bfloat16)
+
+
+def _f32(x):
+    return x if x.dtype == torch.float32 else x.float()
+
+
 def _fast3d(x, conv, bn) -> bool:
-    """Stride-1 'same' Conv3d (+ eval BatchNorm3d) that the halo kernel runs (fp32, no grad)."""
-    if not (FILTER3D and x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
-            and not torch.is_autocast_enabled() and type(conv) is nn.Conv3d):
+    """Stride-1 'same' Conv3d (+ eval BatchNorm3d) that the halo kernel runs (no grad; fp32
+    compute, also under autocast)."""
+    if not (FILTER3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+            and type(conv) is nn.Conv3d):
         return False
     kd, kh, kw = conv.kernel_size
     if conv.stride != (1, 1, 1) or conv.dilation != (1, 1, 1) or conv.groups != 1 or kh != kw or kh not in (1, 3) \
@@ -67,8 +80,8 @@ def _fast3d(x, conv, bn) -> bool:
 
 def _fast2d(x, conv, bn) -> bool:
     """Stride-1 'same' Conv2d (1x1 / 3x3, + eval BatchNorm2d) that the halo kernel runs."""
-    if not (FILTER3D and x.is_cuda and x.dtype == torch.float32 and not torch.is_grad_enabled()
-            and not torch.is_autocast_enabled() and type(conv) is nn.Conv2d):
+    if not (FILTER3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+            and type(conv) is nn.Conv2d):
         return False
     kh, kw = conv.kernel_size
     if conv.stride != (1, 1) or conv.dilation != (1, 1) or conv.groups != 1 or kh != kw or kh not in (1, 3) \
@@ -104,13 +117,14 @@ def _packed_bn(conv, bn):
 def conv2d_bn_act(segs, conv, bn, act=None, **kw):
     """act(bn(conv(cat(segs)))) on the 2D halo kernel (see ``_fast2d``); ``segs`` as ops.conv2d."""
     pk, b = _packed_bn(conv, bn)
+    segs = [_f32(s) if isinstance(s, torch.Tensor) else (_f32(s[0]),) + tuple(s[1:]) for s in segs]
     return ops.conv2d(segs, pk, bias=b, act=act, **kw)
 
 
 def conv3d_bn_act(x, conv, bn, act=None, res=None, res_pre=False):
     """act(bn(conv(x)) [+ res]) on the halo kernel (see ``_fast3d`` for when it applies)."""
     pk, b = _packed_bn(conv, bn)
-    return ops.conv3d(x, pk, bias=b, act=act, res=res, res_pre=res_pre)
+    return ops.conv3d(_f32(x), pk, bias=b, act=act, res=None if res is None else _f32(res), res_pre=res_pre)
 
 
 def _norm(kind, ch, is_3d):
@@ -238,8 +252,20 @@ class FlashMultiheadAttention(nn.Module):
         def heads(t):
             return t.view(B, -1, self.num_heads, self.head_dim).transpose(1, 2)
 
+        mask = None
+        if tuple(window_size) != (-1, -1):
+            # flash_attn_func(window_size=(left, right)) (core/submodule.py:224): query i sees keys
+            # j with i - left <= j <= i + right; -1 leaves that side unbounded
+            left, right = window_size
+            i = torch.arange(L, device=query.device)[:, None]
+            j = torch.arange(key.shape[1], device=query.device)[None, :]
+            mask = torch.ones(L, key.shape[1], dtype=torch.bool, device=query.device)
+            if left >= 0:
+                mask &= j >= i - left
+            if right >= 0:
+                mask &= j <= i + right
         o = F.scaled_dot_product_attention(heads(self.q_proj(query)), heads(self.k_proj(key)),
-                                           heads(self.v_proj(value)))
+                                           heads(self.v_proj(value)), attn_mask=mask)
         return self.out_proj(o.transpose(1, 2).reshape(B, L, C))
 
 
@@ -440,9 +466,9 @@ class CostVolumeDisparityAttention(nn.Module):
                                  for _ in range(num_transformer)])
         self.pos_embed0 = PositionalEmbedding(d_model, max_len=max_len)
 
-    def _fast(self, cv) -> bool:
-        if not (DT_FAST and cv.is_cuda and cv.dtype == torch.float32 and not torch.is_grad_enabled()
-                and not torch.is_autocast_enabled()) or self.training:
+    def _fast(self, cv, window_size=(-1, -1)) -> bool:
+        if not (DT_FAST and cv.is_cuda and cv.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+                and window_size == (-1, -1)) or self.training:
             return False
         a = self.sa[0].self_attn if len(self.sa) else None
         return (a is not None and cv.shape[1] == 28 and a.num_heads == 4 and self.sa[0].linear1.out_features == 28
@@ -462,8 +488,9 @@ class CostVolumeDisparityAttention(nn.Module):
 
     def forward(self, cv, window_size=(-1, -1)):
         B, C, D, H, W = cv.shape
-        if self._fast(cv):
-            # one HIP kernel for PE + all encoder layers (csrc/transformer.hip)
+        if self._fast(cv, tuple(window_size)):
+            # one HIP kernel for PE + all encoder layers (csrc/transformer.hip), fp32
+            cv = _f32(cv)
             pe = self.pos_embed0.pe.to(cv.device, cv.dtype)
             self.pos_embed0.pe = pe
             if pe.shape[1] < D:

@@ -9,11 +9,12 @@ packed once per (module, weight version).  The gates between the convs --
 sigmoid of z/r, ``r*h``, ``cat([r*h, x])``, ``tanh``, ``(1-z)h + zq`` and the
 ``small*att + large*(1-att)`` selection -- are two fused kernels per
 SelectiveConvGRU (``ops.gru_reset``, ``ops.gru_blend``); ``convz`` and
-``convr`` run as ONE conv with stacked weights.  The two 7x7 convs run
-elsewhere: ``convd1`` (1 -> 64) on MIOpen, the depthwise ``dwconv`` on
-``ops.dwconv2d``; ``interp`` is ``ops.resize_bilinear``.  Under autocast or
-with grad enabled the module runs the plain torch path (``CONV_ENGINE =
-"miopen"`` forces it, for A/B).
+``convr`` run as ONE conv with stacked weights.  The two 7x7 convs run on their
+own kernels: ``convd1`` (1 -> 64, + ReLU) on ``ops.conv2d_1in``, the depthwise
+``dwconv`` on ``ops.dwconv2d``; ``pool2x`` is ``ops.pool2x`` and ``interp``
+``ops.resize_bilinear``.  Under the reference's autocast the same HIP path runs
+(fp16 inputs cast up, fp32 compute); with grad enabled the module runs the plain
+torch path (``CONV_ENGINE = "miopen"`` forces it, for A/B).
 """
 from __future__ import annotations
 
@@ -22,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .submodule import EdgeNextConvEncoder
+from .submodule import HIP_DTYPES, EdgeNextConvEncoder, _f32
 
 import os
 
@@ -41,8 +42,14 @@ _POOL_TORCH = os.environ.get("FSMI_POOL_TORCH", "0") == "1"        # A/B knob: t
 
 
 def _fast(x) -> bool:
-    return (CONV_ENGINE == "fsmi" and x.is_cuda and x.dtype == torch.float32
-            and not torch.is_autocast_enabled() and not torch.is_grad_enabled())
+    """The HIP path applies: ROCm tensor, no grad.  Under the reference's autocast
+    (scripts/run_demo.py:161) fp16 / bf16 inputs are cast up and the loop still runs on the HIP
+    kernels in fp32."""
+    return CONV_ENGINE == "fsmi" and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+
+
+def _f32s(xs):
+    return [_f32(x) for x in xs]
 
 
 def _packed(*mods):
@@ -107,7 +114,7 @@ class DispHead(nn.Module):
     def forward(self, x):
         if not _fast(x):
             return self.conv(x)
-        y = _conv(self.conv[0], [x], "relu")
+        y = _conv(self.conv[0], [_f32(x)], "relu")
         for enc in (self.conv[2], self.conv[3]):
             d = ops.dwconv2d(y, enc.dwconv.weight, enc.dwconv.bias)   # depthwise 7x7; norm=None
             e = _conv(enc.pwconv1, [d], "gelu")
@@ -161,6 +168,7 @@ class BasicMotionEncoder(nn.Module):
 
     def forward(self, disp, corr):
         if _fast(corr):
+            corr, disp = _f32(corr), _f32(disp)
             B, _, H, W = corr.shape
             return self.encode_into(disp, corr, corr.new_empty(B, self.conv.out_channels + 1, H, W))
         cor = F.relu(self.convc2(F.relu(self.convc1(corr))))
@@ -171,7 +179,7 @@ class BasicMotionEncoder(nn.Module):
 
 def pool2x(x):
     if _fast(x) and not _POOL_TORCH:
-        return ops.pool2x(x)
+        return ops.pool2x(_f32(x))
     return F.avg_pool2d(x, 3, stride=2, padding=1)
 
 
@@ -181,7 +189,7 @@ def pool4x(x):
 
 def interp(x, dest):
     if _fast(x):
-        return ops.resize_bilinear(x, dest.shape[2:])
+        return ops.resize_bilinear(_f32(x), dest.shape[2:])
     return F.interpolate(x, dest.shape[2:], mode="bilinear", align_corners=True)
 
 
@@ -216,9 +224,12 @@ class RaftConvGRU(nn.Module):
         return _conv((self.convz, self.convr), [hx])
 
     def forward(self, h, x, hx):
-        zr = self.zr_fast(hx) if _fast(hx) else self.zr(hx)
-        qin, _ = ops.gru_reset(zr, zr, h, x)
-        q = _conv(self.convq, [qin]) if _fast(qin) else self.convq(qin)
+        fast = _fast(hx)
+        if fast:
+            h, x, hx = _f32(h), _f32(x), _f32(hx)
+        zr = self.zr_fast(hx) if fast else self.zr(hx).float()
+        qin, _ = ops.gru_reset(zr, zr, h.float(), x.float())
+        q = _conv(self.convq, [qin]) if fast else self.convq(qin).float()
         ones = torch.ones_like(h[:, :1])
         return ops.gru_blend(zr, zr, q, q, h, ones)
 
@@ -236,6 +247,7 @@ class SelectiveConvGRU(nn.Module):
 
     def forward(self, att, h, *x):
         if _fast(h):
+            h, x = _f32(h), _f32s(x)
             xc = _conv(self.conv0[0], list(x), "relu")              # cat(x) as input segments
             hx = _conv(self.conv1[0], [xc, h], "relu")
             # gates in the conv epilogues: z / r*h from the stacked zr convs, then each convq reads
@@ -306,7 +318,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
 
     def forward(self, net, inp, corr, disp, att):
         if _fast(corr):
-            return self._forward_fast(net, inp, corr, disp, att)
+            return self._forward_fast(_f32s(net), _f32s(inp), _f32(corr), _f32(disp), _f32s(att))
         n = self.args.n_gru_layers
         if n == 3:
             net[2] = self.gru16(att[2], net[2], inp[2], pool2x(net[1]))

@@ -230,11 +230,11 @@ int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out,
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
  *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */
+int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,
+                    int H, int W, int relu, void* stream);
 /* fsmi_pool2x: F.avg_pool2d(x, 3, stride=2, padding=1) (count_include_pad) on (B,C,H,W) ->
  *   (B,C,(H-1)/2+1,(W-1)/2+1): pool2x, core/update.py:72-73. */
 int fsmi_pool2x(const float* x, float* out, int B, int C, int H, int W, void* stream);
-int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,
-                    int H, int W, int relu, void* stream);
 
 /* ---- disparity transformer of the hourglass ---------
  * fsmi_dt_patch_embed: conv_patch = depthwise Conv3d(C, C, 4, stride 4) + eval
@@ -278,7 +278,11 @@ int fsmi_timer_query(int kernel, double* total_ms, long long* count);
 int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count);
 /* Re-issue the last timed launch of `kernel` (lookup, cost-volume build) `reps` times back to
  * back on its stream between two hipEvents; *avg_ms = span / reps.  The kernels are pure
- * functions of their inputs, so the replays rewrite identical outputs. */
+ * functions of their inputs, so the replays rewrite identical outputs.
+ * Lifetime contract: the replay reuses the raw device pointers of the recorded launch, so the
+ * CALLER must keep every input and output buffer of that launch allocated until the replay has
+ * finished (ops.py holds references to the last timed launch's tensors until the next
+ * fsmi_timer_reset / fsmi_timer_enable, which also drop the recorded launch). */
 int fsmi_timer_replay(int kernel, int reps, double* avg_ms);
 
 #ifdef __cplusplus

@@ -23,7 +23,7 @@ Params = Dict[str, Tensor]
 __all__ = [
     "groupwise_correlation", "build_gwc_volume", "build_concat_volume",
     "disparity_regression", "context_upsample", "allpairs_corr",
-    "GeoEncoding", "geo_lookup_naive", "oracle_forward", "StageTimer",
+    "GeoEncoding", "geo_lookup_naive", "oracle_forward", "oracle_hierarchical", "input_pad", "StageTimer",
 ]
 
 _BN_EPS = 1e-5
@@ -575,3 +575,51 @@ def oracle_forward(P: Params, args, image1: Tensor, image2: Tensor,
     T.mark(None)
     aux["disp_low"] = disp
     return (up, aux) if return_aux else up
+
+
+def input_pad(ht: int, wd: int, divis_by: int = 32):
+    """InputPadder(dims, mode='sintel', force_square=False)._pad, core/utils/utils.py:19-31:
+    [left, right, top, bottom] replicate padding up to the next multiple of ``divis_by``."""
+    pad_ht = (((ht // divis_by) + 1) * divis_by - ht) % divis_by
+    pad_wd = (((wd // divis_by) + 1) * divis_by - wd) % divis_by
+    return [pad_wd // 2, pad_wd - pad_wd // 2, pad_ht // 2, pad_ht - pad_ht // 2]
+
+
+def _unpad(x: Tensor, pad) -> Tensor:
+    """InputPadder.unpad, core/utils/utils.py:37-41."""
+    ht, wd = x.shape[-2:]
+    return x[..., pad[2]:ht - pad[3], pad[0]:wd - pad[1]]
+
+
+def oracle_hierarchical(P: Params, args, image1: Tensor, image2: Tensor, features, iters: int = 12,
+                        small_ratio: float = 0.5, timer: StageTimer = None, return_aux: bool = False):
+    """FoundationStereo.run_hierachical(test_mode=True), core/foundation_stereo.py:257-274.
+
+    ``features(B, H, W)`` -> ``(feats_left, feats_right, vit_feat)`` is the backbone stand-in at a
+    padded pass resolution (the reference calls ``self.feature`` inside each ``forward``).  Kept
+    as in the reference: bilinear x``small_ratio`` downscale (align_corners False), the coarse
+    pass at the /32-padded small size, unpad, bilinear upsample (align_corners True) scaled by
+    1/small_ratio and clipped at 0, the ``+= _pad[0]`` on the padded init (``:270``, the
+    reference adds the LEFT pad to the disparity value), x0.25 bilinear downscale of it as the
+    1/4-resolution ``init_disp``, then the fine pass -- whose classifier + soft-argmin are still
+    computed and discarded (``:218-220``)."""
+    B, _, H, W = image1.shape
+    s1 = F.interpolate(image1, scale_factor=small_ratio, align_corners=False, mode="bilinear")
+    s2 = F.interpolate(image2, scale_factor=small_ratio, align_corners=False, mode="bilinear")
+    pad = input_pad(*s1.shape[-2:])
+    s1, s2 = (F.pad(x, pad, mode="replicate") for x in (s1, s2))
+    fl, fr, vf = features(B, *s1.shape[-2:])
+    d_small = oracle_forward(P, args, s1, s2, fl, fr, vf, iters=iters, timer=timer)
+    d_small = _unpad(d_small.float(), pad)
+    up = F.interpolate(d_small, size=(H, W), mode="bilinear", align_corners=True) * 1 / small_ratio
+    up = up.clip(0, None)
+    pad = input_pad(H, W)
+    image1, image2, up = (F.pad(x, pad, mode="replicate") for x in (image1, image2, up))
+    up = up + pad[0]
+    init_disp = F.interpolate(up, scale_factor=0.25, mode="bilinear", align_corners=True) * 0.25
+    fl, fr, vf = features(B, *image1.shape[-2:])
+    disp = oracle_forward(P, args, image1, image2, fl, fr, vf, iters=iters, init_disp=init_disp, timer=timer)
+    disp = _unpad(disp.float(), pad)
+    if return_aux:
+        return disp, {"disp_small": d_small, "init_disp": init_disp}
+    return disp

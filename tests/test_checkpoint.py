@@ -11,7 +11,7 @@ from foundationstereo_amd import synth
 from foundationstereo_amd.checkpoint import load_cfg, load_model
 
 
-def _write(tmp_path, vit="vits", cfg_extra=None, drop=None):
+def _write(tmp_path, vit="vits", cfg_extra=None, drop=None, extra=None):
     from foundationstereo_amd.foundation_stereo import FoundationStereo
     args = synth.make_args(max_disp=64, corr_levels=2, vit_size=vit)
     m = FoundationStereo(args)
@@ -19,6 +19,8 @@ def _write(tmp_path, vit="vits", cfg_extra=None, drop=None):
     sd = m.state_dict()
     if drop:
         sd = {k: v for k, v in sd.items() if k != drop}
+    if extra:
+        sd = dict(sd, **extra)
     path = os.path.join(tmp_path, "model_best_bp2.pth")
     torch.save({"model": sd, "global_step": 123, "epoch": 4}, path)
     cfg = dict(args)
@@ -31,7 +33,7 @@ def _write(tmp_path, vit="vits", cfg_extra=None, drop=None):
 def test_load_model_roundtrip(tmp_path):
     path, ref = _write(tmp_path)
     model, meta = load_model(path, overrides={"valid_iters": 8})
-    assert meta == {"global_step": 123, "epoch": 4}
+    assert meta == {"global_step": 123, "epoch": 4, "skipped_backbone_keys": []}
     assert not model.training and model.args.valid_iters == 8 and model.args.get("vit_size") == "vits"
     a, b = model.state_dict(), ref.state_dict()
     assert list(a) == list(b)
@@ -52,4 +54,22 @@ def test_cfg_defaults_vit_size_to_vitl(tmp_path):
 def test_missing_key_is_an_error(tmp_path):
     path, ref = _write(tmp_path, drop="classifier.2.weight")
     with pytest.raises(RuntimeError, match="classifier"):
+        load_model(path)
+
+
+def test_backbone_keys_are_set_aside(tmp_path):
+    """A real checkpoint holds the backbone's ``feature.*`` weights; with the parameter-free
+    synthetic backbone they are reported and everything else still loads strictly."""
+    extra = {"feature.stem.0.weight": torch.zeros(48, 3, 4, 4),
+             "feature.dino.blocks.0.norm1.weight": torch.ones(384)}
+    path, ref = _write(tmp_path, extra=extra)
+    model, meta = load_model(path)
+    assert sorted(meta["skipped_backbone_keys"]) == sorted(extra)
+    a, b = model.state_dict(), ref.state_dict()
+    assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
+
+
+def test_unexpected_non_backbone_key_is_an_error(tmp_path):
+    path, _ = _write(tmp_path, extra={"update_block.bogus.weight": torch.zeros(3)})
+    with pytest.raises(RuntimeError, match="bogus"):
         load_model(path)

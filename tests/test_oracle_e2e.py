@@ -50,3 +50,31 @@ def test_oracle_update_step_matches_reference():
         np.testing.assert_allclose(onet[i].numpy(), g[f"onet{i}"], atol=2e-5, rtol=0)
     np.testing.assert_allclose(mask.numpy(), g["mask"], atol=2e-5, rtol=0)
     np.testing.assert_allclose(delta.numpy(), g["delta"], atol=2e-5, rtol=0)
+
+
+def synth_features(vit, shift):
+    """Backbone stand-in at a pass's padded size (the product's unpreset SyntheticFeature)."""
+    def features(B, H, W):
+        fl, fr, vf = synth.backbone_features(B, H, W, vit, shift_px=shift)
+        return [t(x) for x in fl], [t(x) for x in fr], t(vf)
+    return features
+
+
+def test_oracle_hierarchical_matches_reference():
+    """run_hierachical (core/foundation_stereo.py:257-274) incl. the ``+= _pad[0]`` quirk (_pad[0] = 10
+    at 200x300) vs the reference golden: the coarse pass's padded output and the final disparity."""
+    g = load_golden("hiera_small")
+    H, W, md, iters, L, shift = (int(v) for v in g["meta"])
+    args = synth.make_args(max_disp=md, corr_levels=L, vit_size="vits")
+    P = oracle_params(model_keys(args), seed=1234)
+    left, right = synth.stereo_images(1, H, W)
+    assert oracle.input_pad(H, W)[0] == 10
+    with torch.no_grad():
+        out, aux = oracle.oracle_hierarchical(P, args, t(left), t(right), synth_features("vits", shift), iters=iters,
+                                              return_aux=True)
+    assert out.shape == (1, 1, H, W)
+    pad = oracle.input_pad(H // 2, W // 2)
+    np.testing.assert_allclose(oracle.stereo_oracle._unpad(t(g["disp_small_padded"]), pad).numpy(),
+                               aux["disp_small"].numpy(), atol=1e-3, rtol=0)
+    d = np.abs(out.numpy() - g["disp"]).max()
+    assert d < 1e-3, f"max |dd| = {d} px"

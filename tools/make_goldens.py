@@ -163,10 +163,48 @@ def e2e(fs):
                     json.dump(keys, f)
 
 
+# name: (H, W, max_disp, iters, vit, corr_levels, shift): both passes need /32 padding, so the
+# reference's ``+= padder._pad[0]`` (core/foundation_stereo.py:270) is exercised (_pad[0] = 10)
+HIERA_CASES = {"hiera_small": (200, 300, 64, 4, "vits", 2, 3)}
+
+
+def hiera(fs):
+    """run_hierachical (core/foundation_stereo.py:257-274) with the backbone stand-in synthesising
+    features at each pass's padded size (as the product's SyntheticFeature does unpreset)."""
+    Syn = make_synthetic_feature_class(synth.feature_dims)
+    fs.Feature = Syn
+    for name, (H, W, md, iters, vit, L, shift) in HIERA_CASES.items():
+        args = synth.make_args(max_disp=md, corr_levels=L, vit_size=vit)
+        model = fs.FoundationStereo(args).eval()
+        synth.init_module_(model, seed=1234)
+        model.feature.by_size = (vit, shift)
+        left, right = synth.stereo_images(1, H, W)
+        cap = []
+        orig_fwd = fs.FoundationStereo.forward
+
+        def fwd(self, *a, **k):
+            out = orig_fwd(self, *a, **k)
+            cap.append(out.detach().clone())
+            return out
+
+        fs.FoundationStereo.forward = fwd
+        try:
+            with torch.no_grad():
+                out = model.run_hierachical(t(left), t(right), iters=iters, test_mode=True)
+        finally:
+            fs.FoundationStereo.forward = orig_fwd
+        g = {"disp": out.numpy(), "disp_small_padded": cap[0].numpy(),
+             "meta": np.array([H, W, md, iters, L, shift])}
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **g)
+        print(name, "disp", tuple(out.shape), "mean", float(out.mean()))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fs, sm, geo_mod, up_mod, ut = import_reference()
-    which = sys.argv[1:] or ["ops", "update", "e2e"]
+    which = sys.argv[1:] or ["ops", "update", "e2e", "hiera"]
+    if "hiera" in which:
+        hiera(fs)
     if "ops" in which:
         ops_small(sm, geo_mod, ut)
     if "update" in which:

@@ -86,9 +86,17 @@ def make_synthetic_feature_class(feature_dims_fn):
             super().__init__()
             self.d_out, self.vit_dim = feature_dims_fn(args.vit_size)
             self.preset = None
+            self.by_size = None      # (vit_size, shift_px): synthesise for the input size instead
 
         def forward(self, x):
-            fl, fr, vit = self.preset
+            if self.by_size is not None:
+                from foundationstereo_amd import synth
+                B2, _, H, W = x.shape
+                fl, fr, vit = synth.backbone_features(B2 // 2, H, W, self.by_size[0], shift_px=self.by_size[1])
+                fl, fr, vit = [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr], \
+                    torch.from_numpy(vit)
+            else:
+                fl, fr, vit = self.preset
             out = [torch.cat([a, b], 0) for a, b in zip(fl, fr)]
             return out, torch.cat([vit, vit], 0)
 
