@@ -10,8 +10,9 @@ pairs: cost-volume build, 3D filtering, context net, geometry encoding, 32
 refinement iterations (lookup + ConvGRU update), convex upsampling.  Inputs
 (images and the synthetic backbone's feature maps) are resident
 in HBM before the timed region; the out-of-scope backbone is not run.
-Multi-GPU: the image batch is broadcast from rank 0 every step and the
-disparities all-gathered back (RCCL over xGMI), weights broadcast once.
+Multi-GPU: rank 0 scatters each rank its shard of the image batch every step
+and the disparities are all-gathered back (RCCL over xGMI), weights broadcast
+once.
 
 Rank 0 prints ONE JSON line.  ``roofline`` is the dominant HBM-bound kernel
 (the per-iteration geometry lookup), timed with HIP events on its launch
@@ -92,6 +93,17 @@ def cpu_baseline(args, H, W, iters, threads):
     return dt, T.stages
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,8 +150,8 @@ def main():
     if rank == 0:
         left, right = synth.stereo_images(B, H, W)
         batch = torch.from_numpy(np.stack([left, right], 1)).to(device)
-    else:
-        batch = torch.empty((B, 2, 3, H, W), device=device)
+    else:   # only the shape is read on the receiving ranks: no full-batch buffer
+        batch = torch.empty((1, 1, 1, 1, 1), device=device).expand(B, 2, 3, H, W)
 
     def fn(lft, rgt):
         return model(lft, rgt, iters=iters, test_mode=True)
@@ -276,9 +288,12 @@ def main():
                            "avg_us_kernel_clock": cb_ck_ms * 1e3 / max(cb_ck_n, 1), "launches": cb_n},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(os.cpu_count() or 1, 16)
+        # the host cores this process is given: OMP_NUM_THREADS (16 on the GPU box = its CPU share
+        # per GPU; os.cpu_count() there reports the whole machine, shared with other jobs)
+        threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1)
         dt, stages = cpu_baseline(args, H, W, iters, threads)
         res["cpu_baseline"] = {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+                               "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
                                "sample": f"1 pair of {a.config} (all {iters} iterations) through the fp32 "
                                          f"torch-CPU oracle, {dt:.1f} s",
                                "stages_s": {k: round(v, 3) for k, v in stages.items()}}

@@ -40,11 +40,11 @@ SIGNATURES = {
                     _I, _I, _I, _I, _F, _I, _P],
     "fsmi_conv2d_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _P, _P, _I, _P, _I, _I,
                        _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
-    "fsmi_conv2d_halo_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _P, _P, _I, _P, _I,
+    "fsmi_conv2d_halo_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _P, _P, _P, _I, _P, _I,
                             _I, _I, _I, _I, _I, _I, _I, _F, _I, _I, _P, ctypes.c_longlong, _P],
-    "fsmi_conv2d_halo_x3_gate": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _I, _P, _P, _P,
+    "fsmi_conv2d_halo_x3_gate": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _P, _I, _P, _P, _P,
                                  _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, ctypes.c_longlong, _P],
-    "fsmi_conv3d_halo_x3": [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P,
+    "fsmi_conv3d_halo_x3": [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P,
                             ctypes.c_longlong, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],

@@ -41,17 +41,22 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build_library(force: bool = False, verbose: bool = False, defines=(), variant: str = "") -> str:
+    """Compile every csrc/*.hip and link libfsmi.so.  ``defines`` / ``variant``: an A/B build of
+    the same ABI with extra -D flags, linked to _lib/libfsmi_<variant>.so (load it with FSMI_LIB)."""
+    obj_dir = OBJ if not variant else OBJ + "_" + variant
+    lib = LIB if not variant else os.path.join(LIB_DIR, f"libfsmi_{variant}.so")
+    os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     hdrs = _headers()
     jobs = []
     objs = []
+    dflags = [f"-D{d}" for d in defines]
     for src in _sources():
-        obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src)[:-4] + ".o")
         objs.append(obj)
         if force or _stale(obj, [src] + hdrs):
-            jobs.append([HIPCC, *FLAGS, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *FLAGS, *dflags, "-c", src, "-o", obj])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -64,10 +69,14 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     if jobs:
         with ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
             list(ex.map(run, jobs))
-    if force or jobs or _stale(LIB, objs):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB])
-    return LIB
+    if force or jobs or _stale(lib, objs):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib])
+    return lib
 
 
 if __name__ == "__main__":
-    print(build_library(force="--force" in sys.argv, verbose=True))
+    # python -m foundationstereo_amd.build [--force] [--variant NAME -DMACRO=V ...]
+    argv = sys.argv[1:]
+    variant = argv[argv.index("--variant") + 1] if "--variant" in argv else ""
+    defs = [a[2:] for a in argv if a.startswith("-D")]
+    print(build_library(force="--force" in argv, verbose=True, defines=defs, variant=variant))

@@ -1,0 +1,796 @@
+// Halo-tiled split-precision ("3 x fp16") convolution for the refinement loop.
+//
+// conv2d_x3.hip streams an im2col view: for a 3x3 layer every pixel is staged
+// 9 times and the full weight matrix once per pixel tile (~2.8 GB of on-chip
+// traffic for one 512->512 layer at 120x160).  Here a block owns a 2D pixel
+// tile (TR rows x 32 columns of one image) and BM output channels:
+//   * per 32-channel chunk the (TR+2) x 34 input halo is loaded ONCE, split
+//     into fp16 hi/lo and kept in LDS for all 9 taps (fragments for tap
+//     (dh,dw) are the halo rows/cols shifted by (dh,dw));
+//   * weights (pre-split, pre-packed) either go per tap through a double-
+//     buffered LDS slot whose next fill is in flight during the MFMAs
+//     (conv_halo_x3_kernel, cfg 0/1: one barrier per tap), or each wave loads
+//     its own A fragments from L2 into a double-buffered register set one tap
+//     ahead (conv_halo_wreg_kernel, cfg 2/3: LDS holds only the halo, two
+//     barriers per 32-channel chunk);
+//   * blocks are ordered cout-tile-major over an XCD-aware remap, so each XCD
+//     works on one cout slice and keeps its weights in its 4 MB L2.
+// MFMA v_mfma_f32_32x32x16_f16, three per product (lo*hi, hi*lo, hi*hi), fp32
+// accumulation; fragment maps as in conv2d_x3.hip.  Epilogue identical to
+// fsmi_conv2d (bias, ReLU/GELU, alpha, gamma, residual, channel-offset store).
+//
+// Layout of the sources: this header holds the device code; each (kernel size, 2D / volume)
+// pair compiles in its own translation unit (conv_halo_k{1,3}_{2d,3d}.hip, built in parallel),
+// and conv_halo_x3.hip holds the host side (tile / split-K policy, C ABI) and the reduce pass.
+#pragma once
+#include <cstdlib>
+#include <type_traits>
+
+#include "fsmi_common.h"
+
+#ifndef FSMI_HALO_RANGE
+#define FSMI_HALO_RANGE 1                            // 0: A/B build without the block exponent
+#endif
+// the wreg kernel's lambdas: forced inline only for the 128 x 8 x 32 volume tile, which clang
+// otherwise outlines into a real call; elsewhere the inliner's own order schedules better
+#ifndef FSMI_HALO_FORCE_INLINE
+#define FSMI_HALO_FORCE_INLINE 0
+#endif
+#if FSMI_HALO_FORCE_INLINE
+#define FSMI_HALO_INL __attribute__((always_inline))
+#else
+#define FSMI_HALO_INL
+#endif
+#ifndef FSMI_HALO_PERCOUT
+#define FSMI_HALO_PERCOUT 1                          // 0: A/B build reading one weight scale (row 0's)
+#endif
+
+namespace fsmi {
+namespace halo {
+
+constexpr int kHMaxSeg = 4;        // input segments (zero-copy cat)
+
+struct HaloArgs {
+  const float* seg_ptr[kHMaxSeg];
+  long long seg_bstride[kHMaxSeg];
+  int seg_end[kHMaxSeg];
+  int nseg, Cin, CinP;
+  const _Float16* whi;             // [taps][CinP/32][CoutP][32]
+  const _Float16* wlo;
+  const float2* sb;                // per output channel (2^-wexp[co], bias[co]); weights packed x 2^wexp[co]
+  const float* gamma;
+  const float* res;
+  long long res_bstride;
+  float* out;
+  long long out_bstride;
+  int co0, Cout, CoutP, B, H, W, act;
+  float alpha;
+  int res_pre;                     // residual added before the activation (ResNet block tail)
+  // 3D: NCDHW tensors with D depth planes; a KD x KS x KS kernel is the sum over kd of 2D
+  // convs on plane d + kd - PDD.  2D: D = KD = 1.
+  int D, KD, PDD;
+  long long cstride;               // channel stride = D*H*W
+  int nrt, nct, npix, nco;         // row tiles, col tiles, pixel tiles (B*D*nrt*nct), cout tiles
+  int nsplit, kpc;                 // split-K factor, (kd, channel chunk) pairs per split
+  float* ws;                       // [nsplit][B][Cout][D*H*W] partial sums when nsplit > 1
+  unsigned long long* ts;          // debug (fsmi_debug_conv_timestamps): per-block wall-clock stamps
+  int dbg;                         // ablation (FSMI_CONV_DBG): 1 weights from one line, 2 no halo reloads
+  // SelectiveConvGRU gate epilogues (act 3..5), core/update.py:83-95,117; all (B, gHd, H, W)
+  // except gatt (B, 1, H, W)
+  const float* gh;                 // hidden state h
+  float* gz;                       // z = sigmoid(z_pre): written by act 3, read by act 4 / 5
+  const float* gatt;               // att
+  float* grh;                      // sigmoid(r_pre) * h, written by act 3
+  int gHd;
+};
+
+// Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
+// (D3); defined in conv_halo_k<KS>_<2d|3d>.hip.  Returns FSMI_OK or an error code.
+template <int KS, bool D3>
+int launch_cfg(int cfg, const HaloArgs& a, hipStream_t s);
+
+}  // namespace halo
+
+namespace {
+using halo::HaloArgs;
+using halo::kHMaxSeg;
+
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+constexpr int HKC = 32;            // channels per chunk
+constexpr int HROW = HKC + 8;      // padded LDS row (halves): conflict-free ds_read_b128 at 80-B stride
+
+
+__device__ __forceinline__ float gelu_erf_h(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float sigm_h(float x) { return 1.f / (1.f + expf(-x)); }
+
+// Final value of output channel co at (b, sp) -- sp = d*H*W + h*W + w -- from the conv sum v in
+// packed weight units (x 2^wexp[co]; the split-K partials): v * sb[co].x + sb[co].y, then:
+//  act 0/1/2/6: out[b, co0+co] = res + gamma * alpha * act(v + bias)   (none / ReLU / GELU-erf /
+//               LeakyReLU 0.01); with res_pre: gamma * alpha * act(v + bias + res)
+//  act 3 (convz|convr):  co <  Hd: z[b,co] = sigmoid(v + bias);
+//                        co >= Hd: rh[b,co-Hd] = sigmoid(v + bias) * h[b,co-Hd]
+//  act 4 (small convq):  out[b,co0+co] = ((1-z)h + z tanh(v + bias)) * att
+//  act 5 (large convq):  out[b,co0+co] += ((1-z)h + z tanh(v + bias)) * (1 - att)
+// RESPRE: compile the res_pre (ResNet tail) path; the 2D conv kernels instantiate without it --
+// with the branch present their epilogue needs ~100 more VGPRs (occupancy 2 -> 1).
+// Every tensor arrives as its own __restrict__ parameter: a caller that runs a whole batch of
+// elements inside ONE call of a function taking them so lets the compiler issue all the batch's
+// loads (bias, residual, gate state) ahead of its stores.  Read through the HaloArgs fields
+// (which may alias the output) each load waited behind the previous element's store, and a
+// tile's epilogue paid one L2 round trip per element: 20-56 % of a block's lifetime on the
+// nsplit = 1 layers (tools/conv_phases.py).
+template <bool RESPRE>
+__device__ __forceinline__ void store_el(const HaloArgs& a, float v, int co, int b, long long hw,
+                                         float* __restrict__ out, const float2* __restrict__ sb,
+                                         const float* __restrict__ gamma, const float* __restrict__ res,
+                                         const float* __restrict__ gh, float* __restrict__ gz,
+                                         const float* __restrict__ gatt, float* __restrict__ grh) {
+  const long long HW = a.cstride;
+  {
+    const float2 q = sb[co];       // v: conv sum in packed units (split-K partials)
+    v = v * q.x + q.y;
+  }
+  if (a.act >= 3 && a.act <= 5) {
+    const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
+    if (a.act == 3) {
+      const float sg = sigm_h(v);
+      if (co < a.gHd) gz[g] = sg;
+      else grh[g] = sg * gh[g];
+      return;
+    }
+    const float z = gz[g], hv = gh[g], at = gatt[static_cast<size_t>(b) * HW + hw];
+    const float hn = (1.f - z) * hv + z * tanhf(v);
+    float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+    if (a.act == 4) *o = hn * at;
+    else *o = *o + hn * (1.f - at);
+    return;
+  }
+  float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+  if (RESPRE && a.res_pre) {       // ResNet tail: act(v + bias + res)
+    v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
+    *o = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v);
+    return;
+  }
+  if (a.act == 1) v = fmaxf(v, 0.f);
+  else if (a.act == 2) v = gelu_erf_h(v);
+  else if (a.act == 6) v = v >= 0.f ? v : 0.01f * v;
+  v *= a.alpha;
+  if (gamma) v *= gamma[co];
+  if (res) v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
+  *o = v;
+}
+
+template <bool RESPRE = true>
+__device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, int b, long long hw) {
+  store_el<RESPRE>(a, v, co, b, hw, a.out, a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh);
+}
+
+// One 16-element accumulator fragment (couts cb + (r&3) + 8(r>>2)) at one pixel, activation ACT
+// fixed at compile time and one restrict scope: the fragment's bias / gamma / residual / gate
+// loads are issued together, then 16 branch-free finishes and stores.  (The generic store_el per
+// element compiled to ~400 instructions per fragment with a wait per element: 20-56 % of a
+// block's lifetime went to the epilogue on the nsplit = 1 layers, tools/conv_phases.py.)
+template <int ACT, bool RESPRE>
+__device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, float xinv, int cb, int b,
+                                           long long hw, float* __restrict__ out, const float2* __restrict__ sb,
+                                           const float* __restrict__ gamma, const float* __restrict__ res,
+                                           const float* __restrict__ gh, float* __restrict__ gz,
+                                           const float* __restrict__ gatt, float* __restrict__ grh) {
+  const long long HW = a.cstride;
+  float2 q[16];                    // (weight scale 2^-wexp[co], bias[co]) of the 16 rows
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    q[r] = sb[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)];
+    q[r].x *= xinv;
+  }
+  if constexpr (ACT >= 3 && ACT <= 5) {
+    const float at = ACT == 3 ? 0.f : gatt[static_cast<size_t>(b) * HW + hw];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = cb + (r & 3) + 8 * (r >> 2);
+      if (co >= a.Cout) continue;
+      const float x = v[r] * q[r].x + q[r].y;
+      const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
+      if constexpr (ACT == 3) {
+        const float sg = sigm_h(x);
+        if (co < a.gHd) gz[g] = sg;
+        else grh[g] = sg * gh[g];
+      } else {
+        const float z = gz[g];
+        const float hn = (1.f - z) * gh[g] + z * tanhf(x);
+        float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+        if constexpr (ACT == 4) *o = hn * at;
+        else *o = *o + hn * (1.f - at);
+      }
+    }
+    return;
+  } else {
+    float gv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gv[r] = gamma ? gamma[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)] : 1.f;
+    const bool pre = RESPRE && a.res_pre;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = cb + (r & 3) + 8 * (r >> 2);
+      if (co >= a.Cout) continue;
+      float x = v[r] * q[r].x + q[r].y;
+      const float rv = res ? res[b * a.res_bstride + static_cast<long long>(co) * HW + hw] : 0.f;
+      if (pre) x += rv;            // ResNet tail: act(conv + bias + res)
+      if constexpr (ACT == 1) x = fmaxf(x, 0.f);
+      else if constexpr (ACT == 2) x = gelu_erf_h(x);
+      else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
+      if (!pre) x = x * a.alpha * gv[r] + rv;
+      out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw] = x;
+    }
+  }
+}
+
+// 4 consecutive pixels of one channel, one restrict scope
+__device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], int co, int b, long long hw,
+                                       float* __restrict__ out, const float2* __restrict__ sb,
+                                       const float* __restrict__ gamma, const float* __restrict__ res,
+                                       const float* __restrict__ gh, float* __restrict__ gz,
+                                       const float* __restrict__ gatt, float* __restrict__ grh) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) store_el<true>(a, v[k], co, b, hw + k, out, sb, gamma, res, gh, gz, gatt, grh);
+}
+
+// ---------------------------------------------------------------- shared pieces
+
+// Input-halo staging for a TR x 32 pixel tile: task = (halo pixel, 8-channel
+// group); per task a packed descriptor (clamped pixel offset << 3 | in-image << 2
+// | group) computed once per block; a chunk is loaded into registers one chunk
+// ahead and split into fp16 hi/lo when stored to LDS.
+template <int KS, int TR>
+struct HaloStage {
+  static constexpr int PD = KS / 2, HR = TR + KS - 1, HC = 32 + KS - 1, NHP = HR * HC;
+  static constexpr int X_TASKS = NHP * (HKC / 8), X_PER_T = (X_TASKS + 255) / 256;
+  int desc[X_PER_T];
+  f32x8 xv[X_PER_T];
+
+  __device__ __forceinline__ void init(const HaloArgs& a, int tid, int r0, int c0) {
+#pragma unroll
+    for (int u = 0; u < X_PER_T; ++u) {
+      const int task = min(tid + 256 * u, X_TASKS - 1);
+      const int hp = task % NHP, g = task / NHP;
+      const int hr = hp / HC, hc = hp - hr * HC;
+      const int hh = r0 + hr - PD, ww = c0 + hc - PD;
+      const bool in = hh >= 0 && hh < a.H && ww >= 0 && ww < a.W && tid + 256 * u < X_TASKS;
+      const int pix = min(max(hh, 0), a.H - 1) * a.W + min(max(ww, 0), a.W - 1);
+      desc[u] = (pix << 3) | (in ? 4 : 0) | g;
+    }
+  }
+
+  // chunk cc of depth plane d (zeros outside [0, D))
+  __device__ __forceinline__ void load(const HaloArgs& a, int b, int cc, int d = 0) {
+    const long long HW = a.cstride;
+    const bool full = (cc + 1) * HKC <= a.Cin;     // block-uniform: only the last chunk is ragged
+    const bool plane_ok = d >= 0 && d < a.D;
+    const long long poff = static_cast<long long>(min(max(d, 0), a.D - 1)) * a.H * a.W;
+#pragma unroll
+    for (int u = 0; u < X_PER_T; ++u) {
+      const int g = desc[u] & 3, pix = desc[u] >> 3;
+      const int ci0 = cc * HKC + g * 8;
+      const int cic = min(ci0, a.Cin - 1);
+      // segment of this 8-channel group (segments hold multiples of 8 channels): a select
+      // chain over constant indices, so the kernarg arrays are never indexed per lane
+      const float* sp = a.seg_ptr[0];
+      long long sb = a.seg_bstride[0];
+      int base = 0;
+#pragma unroll
+      for (int q = 1; q < kHMaxSeg; ++q) {
+        const bool in_q = q < a.nseg && cic >= a.seg_end[q - 1];
+        sp = in_q ? a.seg_ptr[q] : sp;
+        sb = in_q ? a.seg_bstride[q] : sb;
+        base = in_q ? a.seg_end[q - 1] : base;
+      }
+      const float* src = sp + b * sb + static_cast<long long>(cic - base) * HW + poff + pix;
+      const bool ok = (desc[u] & 4) && plane_ok;
+      f32x8 v;
+      if (full) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = src[static_cast<size_t>(j) * HW];
+      } else {
+        const int nv = a.Cin - ci0;                // may be <= 0 in the padded tail
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = src[static_cast<size_t>(max(0, min(j, nv - 1))) * HW];
+          v[j] = j < nv ? t : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[u][j] = ok ? v[j] : 0.f;
+    }
+  }
+
+  // largest |x| of the chunk this thread holds (zero padding included; NaN ignored here, it still
+  // propagates through the products)
+  __device__ __forceinline__ float absmax() const {
+    float m = 0.f;
+#pragma unroll
+    for (int u = 0; u < X_PER_T; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(xv[u][j]));
+    return m;
+  }
+
+  // split x * 2^s (scale = 2^s, the block's chunk exponent) into fp16 hi + lo
+  __device__ __forceinline__ void store(_Float16 (*Xh)[HROW], _Float16 (*Xl)[HROW], int tid, float scale) const {
+#pragma unroll
+    for (int u = 0; u < X_PER_T; ++u) {
+      const int task = tid + 256 * u;
+      if (X_TASKS % 256 == 0 || task < X_TASKS) {
+        const int hp = task % NHP, g = task / NHP;
+        const f32x8 x = xv[u] * scale;
+        const half8 hi = __builtin_convertvector(x, half8);
+        const half8 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x8), half8);
+        *reinterpret_cast<half8*>(&Xh[hp][g * 8]) = hi;
+        *reinterpret_cast<half8*>(&Xl[hp][g * 8]) = lo;
+      }
+    }
+  }
+};
+
+struct TileCoord {
+  int m0, b, d0, r0, c0, split;
+};
+
+// ---- range-safe split: a block exponent per 32-channel chunk
+// fp16 hi / lo halves hold x to ~22 bits only while |x| < 65504 and x's low half stays normal
+// (|x| >~ 0.1).  Before a chunk is split, the block takes the largest |x| of the chunk (wave
+// reduce + one LDS slot per wave, read after the staging barrier the kernel has anyway) and
+// scales the chunk by 2^s so that max|x| * 2^s lies in [2^14, 2^15): the hi halves never overflow
+// and every value within 2^-17 of the chunk maximum keeps its full 22 bits.  s only decreases
+// over a block's chunks; when it does, the fp32 accumulators are rescaled by the exact power of
+// two, and the epilogue multiplies by 2^-s.  Values far below the chunk maximum lose low bits
+// only at ~2^-40 of that maximum -- below the fp32 rounding of the sum they are added to.
+constexpr int kNoExp = 127;                          // no chunk seen yet / all-zero chunks
+
+// max over the wave of v >= 0: DPP row shifts within each 16-lane row, then the row_bcast:15 /
+// row_bcast:31 steps of the GFX9 scan idiom (all VALU, no LDS round trip); lane 63 ends with the
+// wave max, read into an SGPR.  Lanes without a DPP source read 0, harmless for a max of v >= 0.
+__device__ __forceinline__ float wave_max(float v) {
+  int x = __float_as_int(v);
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false))));
+  x = __float_as_int(fmaxf(__int_as_float(x), __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false))));
+  return __int_as_float(__builtin_amdgcn_readlane(x, 63));
+}
+
+__device__ __forceinline__ float exp2i(int e) {     // 2^e for e in [-126, 127], exact
+  return __uint_as_float(static_cast<unsigned>(e + 127) << 23);
+}
+
+// target exponent for a chunk whose largest |x| is m (kNoExp when m == 0)
+__device__ __forceinline__ int chunk_exp(float m) {
+  if (!(m > 0.f)) return kNoExp;
+  const int e = static_cast<int>((__float_as_uint(m) >> 23) & 0xff) - 127;   // floor(log2 m); m < 2^-126 -> -127
+  return min(max(14 - e, -126), 126);
+}
+
+__device__ __forceinline__ float red4_max(const float* red) {
+  const float4 r = *reinterpret_cast<const float4*>(red);       // one ds_read_b128
+  return fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w));
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void rescale_acc(f32x16 (&acc)[TM][TN], float f) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] *= f;
+}
+
+// Tile t (cout tile = t / npix, pixel tile = t % npix; D3: depth fastest) -> coordinates
+template <int BM, int TR, bool D3>
+__device__ __forceinline__ TileCoord tile_coord(const HaloArgs& a, int ctile, int ptile) {
+  TileCoord t;
+  t.split = 0;
+  t.m0 = ctile * BM;
+  const int per_plane = a.nrt * a.nct;
+  int prem;
+  if constexpr (D3) {
+    // depth fastest: blocks of consecutive output depths at one (row, col) tile run together on
+    // one XCD, so the KD input planes each of them reads are shared in that XCD's L2 (depth-
+    // slowest order re-fetched them from HBM: 10x the input for a (17,1,1) conv)
+    t.d0 = ptile % a.D;
+    const int rest = ptile / a.D;
+    t.b = rest / per_plane;
+    prem = rest - t.b * per_plane;
+  } else {
+    t.b = ptile / per_plane;
+    t.d0 = 0;
+    prem = ptile - t.b * per_plane;
+  }
+  t.r0 = (prem / a.nct) * TR;
+  t.c0 = (prem % a.nct) * 32;
+  return t;
+}
+
+// cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
+template <int BM, int TR, bool D3>
+__device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int cs = item / a.npix;                    // (cout tile, split) pair
+  const int ptile = item - cs * a.npix;
+  const int ctile = cs / a.nsplit;
+  TileCoord t = tile_coord<BM, TR, D3>(a, ctile, ptile);
+  t.split = cs - ctile * a.nsplit;
+  return t;
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM], const half8 (&al)[TM],
+                                     const half8 (&bh)[TN], const half8 (&bl)[TN]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// Non-split epilogue of the block's tile with the activation fixed at compile time
+template <int ACT, int TM, int TN, bool D3>
+__device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv, const TileCoord& t,
+                                         int wm, int wn, int lane) {
+  const int hsel = lane >> 5, rl = lane & 31;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
+    if (hh >= a.H || ww >= a.W) continue;
+    const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      store_frag<ACT, D3>(a, acc[i][j], xinv, t.m0 + (wm * TM + i) * 32 + 4 * hsel, t.b, hw, a.out, a.sb, a.gamma,
+                          a.res, a.gh, a.gz, a.gatt, a.grh);
+  }
+}
+
+// n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
+template <int TM, int TN, bool D3>
+__device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv,
+                                              const TileCoord& t, int wm, int wn, int lane, bool partial) {
+  const int hsel = lane >> 5, rl = lane & 31;
+  const long long HW = a.cstride;
+  if (partial) {                   // raw partial sums into ws slot t.split; a reduce applies the epilogue
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
+      if (hh >= a.H || ww >= a.W) continue;
+      const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
+      float* wp = a.ws + (static_cast<size_t>(t.split) * a.B + t.b) * a.Cout * HW + hw;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+          if (co < a.Cout) wp[static_cast<size_t>(co) * HW] = acc[i][j][r] * xinv;   // packed units
+        }
+    }
+    return;
+  }
+  switch (a.act) {                 // uniform: one specialised tile epilogue per activation
+    case 1: epi_tile<1, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    case 2: epi_tile<2, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    case 3: epi_tile<3, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    case 4: epi_tile<4, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    case 5: epi_tile<5, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    case 6: epi_tile<6, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    default: epi_tile<0, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+  }
+}
+
+// ---------------------------------------------------------------- cfg 0/1: weights through LDS
+
+template <int KS, int BM, int TR, int WM, bool D3>
+__global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32, TN = TR / WN;
+  constexpr int NTAP = KS * KS;
+  constexpr int W_PIECES = BM * HKC / 8;           // 16-B pieces per hi (or lo) weight slice
+  constexpr int W_PER_T = W_PIECES / 256;
+  static_assert(W_PIECES % 256 == 0, "weight pieces must tile the block");
+  using HS = HaloStage<KS, TR>;
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Wh[2][BM][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Wl[2][BM][HROW];
+  __shared__ __attribute__((aligned(16))) float red[4];   // per-wave chunk max |x| (block exponent)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int hsel = lane >> 5, rl = lane & 31;
+  const TileCoord tc = decode_tile<BM, TR, D3>(a);
+  const int m0 = tc.m0;
+  const int nck = a.CinP / HKC;
+  const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
+
+  const bool w_full = m0 + BM <= a.CoutP;          // block-uniform: only the last cout tile is ragged
+  uint4 rwh[W_PER_T], rwl[W_PER_T];
+  auto load_w = [&](int cc, int tap) {
+    const size_t base = D3 ? (static_cast<size_t>((cc / nck) * NTAP + tap) * nck + cc % nck) * a.CoutP * HKC
+                           : (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+    const _Float16* ph = a.whi + base;
+    const _Float16* pl = a.wlo + base;
+    if (w_full) {
+#pragma unroll
+      for (int u = 0; u < W_PER_T; ++u) {
+        const int e = tid + 256 * u;
+        const int off = (m0 + e / (HKC / 8)) * HKC + (e % (HKC / 8)) * 8;
+        rwh[u] = *reinterpret_cast<const uint4*>(ph + off);
+        rwl[u] = *reinterpret_cast<const uint4*>(pl + off);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < W_PER_T; ++u) {
+        const int e = tid + 256 * u;
+        const int row = m0 + e / (HKC / 8);
+        const int off = min(row, a.CoutP - 1) * HKC + (e % (HKC / 8)) * 8;   // clamped, then zeroed
+        const uint4 h = *reinterpret_cast<const uint4*>(ph + off);
+        const uint4 l = *reinterpret_cast<const uint4*>(pl + off);
+        const bool ok = row < a.CoutP;             // per component: a uint4 ternary goes via scratch
+        rwh[u] = make_uint4(ok ? h.x : 0u, ok ? h.y : 0u, ok ? h.z : 0u, ok ? h.w : 0u);
+        rwl[u] = make_uint4(ok ? l.x : 0u, ok ? l.y : 0u, ok ? l.z : 0u, ok ? l.w : 0u);
+      }
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < W_PER_T; ++u) {
+      const int e = tid + 256 * u;
+      const int m = e / (HKC / 8), q = e % (HKC / 8);
+      *reinterpret_cast<uint4*>(&Wh[buf][m][q * 8]) = rwh[u];
+      *reinterpret_cast<uint4*>(&Wl[buf][m][q * 8]) = rwl[u];
+    }
+  };
+  HS hs;
+  hs.init(a, tid, tc.r0, tc.c0);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // split-K: this block reduces chunks [cc_begin, cc_end)
+  const int cc_begin = tc.split * a.kpc;
+  const int cc_end = min(nq, cc_begin + a.kpc);
+  int step = 0;
+  load_w(cc_begin, 0);
+  if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
+  else hs.load(a, tc.b, cc_begin);
+  int sx = kNoExp;                 // block exponent of the split (see chunk_exp)
+  for (int cc = cc_begin; cc < cc_end; ++cc) {
+    if constexpr (FSMI_HALO_RANGE) {
+      const float m = wave_max(hs.absmax());
+      if (lane == 0) red[wave] = m;           // m is wave-uniform (SGPR)
+    }
+    __syncthreads();               // every wave is done with the previous chunk's halo; maxima visible
+    if constexpr (FSMI_HALO_RANGE) {
+      const int se = __builtin_amdgcn_readfirstlane(
+          chunk_exp(red4_max(red)));     // block-uniform
+      if (se < sx) {
+        if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
+        sx = se;
+      }
+    }
+    hs.store(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx));
+    if (cc + 1 < cc_end) {
+      if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
+      else hs.load(a, tc.b, cc + 1);
+    }   // in flight during this chunk's taps
+#pragma unroll 1
+    for (int tap = 0; tap < NTAP; ++tap, ++step) {
+      const int buf = step & 1;
+      store_w(buf);
+      __syncthreads();             // halo (first tap) and this tap's weights visible
+      // next slice; past the end it re-loads the last one (unconditional, never used)
+      const bool wrap = tap + 1 == NTAP;
+      load_w(wrap ? min(cc + 1, cc_end - 1) : cc, wrap ? 0 : tap + 1);
+      const int dh = tap / KS, dw = tap % KS;
+#pragma unroll
+      for (int ks = 0; ks < HKC; ks += 16) {
+        half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = (wm * TM + i) * 32 + rl;
+          ah[i] = *reinterpret_cast<const half8*>(&Wh[buf][m][ks + 8 * hsel]);
+          al[i] = *reinterpret_cast<const half8*>(&Wl[buf][m][ks + 8 * hsel]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+          bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][ks + 8 * hsel]);
+          bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][ks + 8 * hsel]);
+        }
+        mma3<TM, TN>(acc, ah, al, bh, bl);
+      }
+    }
+  }
+  conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1);
+}
+
+// ---------------------------------------------------------------- cfg 2/3: weights in registers
+
+template <int KS, int BM, int TR, int WM, bool D3>
+__global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32, TN = TR / WN;
+  constexpr int NTAP = KS * KS;
+  using HS = HaloStage<KS, TR>;
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) float red[4];   // per-wave chunk max |x| (block exponent)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int hsel = lane >> 5, rl = lane & 31;
+  const int nck = a.CinP / HKC;
+  const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
+  unsigned long long* tsb = a.ts ? a.ts + static_cast<size_t>(blockIdx.x) * 40 : nullptr;
+  if (tsb && tid == 0) tsb[0] = wall_clock64();
+
+  // one segment: chunks [cc_begin, cc_end) of tile tc; partial: raw sums into ws slot tc.split
+  auto segment = [&](const TileCoord& tc, int cc_begin, int cc_end, bool partial) FSMI_HALO_INL {
+    // this lane's A-fragment rows (rows past Cout only feed outputs the epilogue drops:
+    // clamped so every address is mapped, no zeroing needed)
+    int wrow[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) wrow[i] = min(tc.m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
+    half8 wf[2][TM][2][2];         // [buffer][i][k half][hi, lo]
+    auto load_wf = [&](auto buf_c, int cc, int tap) FSMI_HALO_INL {
+      constexpr int buf = decltype(buf_c)::value;
+      size_t base = D3 ? (static_cast<size_t>((cc / nck) * NTAP + tap) * nck + cc % nck) * a.CoutP * HKC
+                       : (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+      if (a.dbg & 1) base = 0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
+          wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+        }
+    };
+    HS hs;
+    hs.init(a, tid, tc.r0, tc.c0);
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
+    auto chunk = [&](auto par_c, int cc) FSMI_HALO_INL {
+      constexpr int P = decltype(par_c)::value;
+#pragma unroll
+      for (int tap = 0; tap < NTAP; ++tap) {
+        const bool last = tap + 1 == NTAP;
+        if (((tap + P) & 1) == 0) {
+          load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+        } else {
+          load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+        }
+        // issue the next tap's loads before this tap's MFMAs: unfenced, the scheduler sinks them
+        // below the last MFMA and reuses the current buffer's registers -- a single buffer whose
+        // L2 round trip every tap then waits on
+        __builtin_amdgcn_sched_barrier(0);
+        const int dh = tap / KS, dw = tap % KS;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            ah[i] = wf[(tap + P) & 1][i][k][0];
+            al[i] = wf[(tap + P) & 1][i][k][1];
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+            bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][16 * k + 8 * hsel]);
+            bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][16 * k + 8 * hsel]);
+          }
+          mma3<TM, TN>(acc, ah, al, bh, bl);
+        }
+        // keep the one-tap-ahead structure: without this fence the scheduler hoists every
+        // tap's loads of the unrolled chunk to its top (500 registers, 1 wave per SIMD)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    int sx = kNoExp;               // block exponent of the segment (see chunk_exp)
+    auto stage = [&](int cc) FSMI_HALO_INL {
+      if constexpr (FSMI_HALO_RANGE) {
+        const float m = wave_max(hs.absmax());
+        if (lane == 0) red[wave] = m;
+      }
+      __syncthreads();             // every wave is done with the previous chunk's halo; maxima visible
+      if (tsb && tid == 0 && cc - cc_begin < 36) tsb[1 + cc - cc_begin] = wall_clock64();
+      if constexpr (FSMI_HALO_RANGE) {
+        const int se = __builtin_amdgcn_readfirstlane(
+            chunk_exp(red4_max(red)));   // block-uniform
+        if (se < sx) {
+          if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
+          sx = se;
+        }
+      }
+      hs.store(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx));
+      if (cc + 1 < cc_end && !(a.dbg & 2)) {
+        if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
+        else hs.load(a, tc.b, cc + 1);
+      }   // in flight during this chunk's taps
+      __syncthreads();
+    };
+    load_wf(std::integral_constant<int, 0>(), cc_begin, 0);
+    if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
+    else hs.load(a, tc.b, cc_begin);
+    // chunks in pairs so every register-buffer index is static (parity 0, then 1)
+    int cc = cc_begin;
+    for (; cc + 1 < cc_end; cc += 2) {
+      stage(cc);
+      chunk(std::integral_constant<int, 0>(), cc);
+      stage(cc + 1);
+      chunk(std::integral_constant<int, 1>(), cc + 1);
+    }
+    if (cc < cc_end) {
+      stage(cc);
+      chunk(std::integral_constant<int, 0>(), cc);
+    }
+    if (tsb && tid == 0) tsb[37] = wall_clock64();
+    conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, partial);
+    if (tsb && tid == 0) {
+      tsb[38] = wall_clock64();
+      tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
+    }
+  };
+
+  const TileCoord tc = decode_tile<BM, TR, D3>(a);
+  const int c0 = tc.split * a.kpc;
+  segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
+}
+
+template <int KS, int BM, int TR, int WM, bool WREG, bool D3>
+void launch_tile(const HaloArgs& a, hipStream_t s) {
+  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
+  if constexpr (WREG) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);
+}
+
+}  // namespace
+}  // namespace fsmi
+
+// tiles = couts x (rows x 32 px), as listed in conv_halo_x3.hip's tile_counts switch
+#define FSMI_HALO_LAUNCH_CFG(KS, D3)                                                       \
+  namespace fsmi {                                                                          \
+  namespace halo {                                                                          \
+  template <>                                                                               \
+  int launch_cfg<KS, D3>(int cfg, const HaloArgs& a, hipStream_t s) {                      \
+    switch (cfg) {                                                                          \
+      case 0: launch_tile<KS, 64, 8, 1, false, D3>(a, s); break;                            \
+      case 1: launch_tile<KS, 128, 4, 2, false, D3>(a, s); break;                           \
+      case 2: launch_tile<KS, 64, 8, 1, true, D3>(a, s); break;                             \
+      case 3: launch_tile<KS, 128, 4, 2, true, D3>(a, s); break;                            \
+      case 4: launch_tile<KS, 128, 2, 2, true, D3>(a, s); break;                            \
+      case 5: launch_tile<KS, 64, 4, 1, true, D3>(a, s); break;                             \
+      case 6: launch_tile<KS, 32, 8, 1, true, D3>(a, s); break;                             \
+      case 8: launch_tile<KS, 128, 8, 2, true, D3>(a, s); break;                            \
+      case 9: launch_tile<KS, 256, 4, 4, true, D3>(a, s); break;                            \
+      default: launch_tile<KS, 32, 4, 1, true, D3>(a, s); break;                            \
+    }                                                                                       \
+    return finish_launch("fsmi_conv_halo");                                                 \
+  }                                                                                         \
+  }                                                                                         \
+  }

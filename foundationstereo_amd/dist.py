@@ -7,9 +7,9 @@ per-iteration communication.  The only exchanges are real data movement:
 1. ``broadcast_module_``: rank 0's weights to every rank, once, as ONE
    flattened fp32 buffer per dtype (one RCCL broadcast over xGMI instead of
    ~700 small ones);
-2. ``ShardedStereo.step``: the input batch is broadcast from rank 0 (the rank
-   that owns the request queue); rank k runs pairs ``[k*b, (k+1)*b)``; the
-   disparities come back with one ``all_gather_into_tensor``.
+2. ``ShardedStereo.step``: rank 0 (the rank that owns the request queue)
+   scatters the pairs -- rank k receives only its pairs ``[k*b, (k+1)*b)`` --
+   and the disparities come back with one ``all_gather_into_tensor``.
 
 One process per GPU, ``torch.distributed`` with backend "nccl" (= RCCL on
 ROCm); the same code runs on "gloo" for the CPU tests.
@@ -59,6 +59,8 @@ def broadcast_module_(module: torch.nn.Module, src: int = 0):
         by_dtype.setdefault(t.dtype, []).append(t)
     for dtype, ts in sorted(by_dtype.items(), key=lambda kv: str(kv[0])):
         flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        if _host_staged():
+            flat = flat.cpu()
         dist.broadcast(flat, src=src)
         off = 0
         for t in ts:
@@ -68,51 +70,84 @@ def broadcast_module_(module: torch.nn.Module, src: int = 0):
     return module
 
 
-class ShardedStereo:
-    """Run ``fn(left, right) -> disp`` on this rank's shard of a broadcast batch.
+def _host_staged() -> bool:
+    """gloo collectives take host tensors (the CPU tests, and multi-process GPU tests that share
+    one device); RCCL ("nccl") moves device memory directly over xGMI."""
+    return dist.get_backend() == "gloo"
 
-    ``batch`` (shape ``(B, 2, 3, H, W)``, identical on every rank after the
-    broadcast) holds [left, right] per pair; every rank must get the same B
-    and ``B % world == 0`` so the gather is a single equal-size collective.
+
+class ShardedStereo:
+    """Run ``fn(left, right) -> disp`` on this rank's shard of a batch held by rank 0.
+
+    Per step, rank 0 SCATTERS the pairs (``batch`` of shape ``(B, 2, 3, H, W)``, [left, right]
+    per pair): rank k receives only its ``B / world`` pairs ``[k*b, (k+1)*b)`` into a
+    persistent local buffer (1/world of the bytes a broadcast would move to every rank), runs
+    them, and the disparities come back with ONE all-gather (every rank ends with the full,
+    ordered batch).  ``B % world == 0`` so both collectives are equal-size.  Non-zero ranks may
+    pass any tensor of the batch's shape and dtype (only its shape is used).
     """
 
     def __init__(self, fn: Callable, rank: int, world: int):
         self.fn = fn
         self.rank = rank
         self.world = world
-        self._graph = None          # (hipGraph, static output, input key) after capture()
+        self._local = None          # this rank's shard, (b, 2, 3, H, W), fixed storage
+        self._graph = None          # (hipGraph, static output) after capture()
+
+    def _local_buffer(self, batch):
+        b = batch.shape[0] // self.world
+        shape = (b,) + tuple(batch.shape[1:])
+        if self._local is None or tuple(self._local.shape) != shape or self._local.device != batch.device:
+            self._local = torch.empty(shape, device=batch.device, dtype=batch.dtype)
+            self._graph = None
+        return self._local
+
+    def _scatter(self, batch):
+        """rank 0's batch -> every rank's local buffer (no collective at world 1)."""
+        local = self._local_buffer(batch)
+        if not (self.world > 1 and dist.is_initialized()):
+            local.copy_(batch)
+            return local
+        host = _host_staged()
+        chunks = None
+        if self.rank == 0:
+            chunks = list((batch.cpu() if host else batch).chunk(self.world, 0))
+            chunks = [c.contiguous() for c in chunks]
+        recv = torch.empty(local.shape, dtype=local.dtype) if host else local
+        dist.scatter(recv, scatter_list=chunks, src=0)
+        if host:
+            local.copy_(recv)
+        return local
 
     def capture(self, batch: torch.Tensor):
-        """Capture this rank's forward on ``batch`` (fixed storage) into a hipGraph;
-        later ``step`` calls on the same tensor replay it.  The broadcast and the
-        gather stay outside the graph.  Warm up eagerly first (MIOpen find,
-        weight packing, workspaces)."""
-        lo, hi = shard_range(batch.shape[0], self.rank, self.world)
-        local = batch[lo:hi]
+        """Capture this rank's forward on its local shard buffer (fixed storage) into a hipGraph;
+        later ``step`` calls scatter into that buffer and replay.  The scatter and the gather
+        stay outside the graph.  Warm up eagerly first (MIOpen find, weight packing, workspaces)."""
+        local = self._local_buffer(batch)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = self.fn(local[:, 0], local[:, 1])
-        self._graph = (g, out, (batch.data_ptr(), tuple(batch.shape)))
+        self._graph = (g, out)
 
-    def _local(self, batch, lo, hi):
-        if self._graph is not None and self._graph[2] == (batch.data_ptr(), tuple(batch.shape)):
+    def _run(self, local):
+        if self._graph is not None:
             self._graph[0].replay()
             return self._graph[1]
-        local = batch[lo:hi]
         return self.fn(local[:, 0], local[:, 1])
 
     def step(self, batch: torch.Tensor, out_shape_per_pair: Tuple[int, ...]) -> torch.Tensor:
         B = batch.shape[0]
         if B % self.world:
             raise ValueError(f"batch {B} not divisible by world size {self.world}")
-        distributed = self.world > 1 and dist.is_initialized()
-        if distributed:
-            dist.broadcast(batch, src=0)
-        lo, hi = shard_range(B, self.rank, self.world)
-        disp = self._local(batch, lo, hi)
-        if not distributed:
+        local = self._scatter(batch)
+        disp = self._run(local)
+        if not (self.world > 1 and dist.is_initialized()):
             return disp
+        if _host_staged():
+            parts = [torch.empty_like(disp, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, disp.contiguous().cpu())
+            return torch.cat(parts, 0).to(disp.device)
         gathered = torch.empty((B,) + tuple(out_shape_per_pair), device=disp.device, dtype=disp.dtype)
         dist.all_gather_into_tensor(gathered, disp.contiguous())
         return gathered

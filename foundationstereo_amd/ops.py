@@ -311,14 +311,37 @@ class PackedConv:
         self.wexp = 0 if amax == 0 else -int(math.floor(math.log2(amax)))   # max |w| * 2^wexp in [1, 2)
         cinp = (self.cin + 31) // 32 * 32
         coutp = (self.cout + 31) // 32 * 32
+        if mode == "halo":
+            # per output channel: row max |w| * 2^e[co] in [1, 2) -- BN folding spreads the rows'
+            # scales over decades, and a per-tensor exponent would leave the small rows' lo halves
+            # fp16-subnormal (~11-bit weights).  The kernel multiplies row co by wscale[co] = 2^-e[co].
+            rmax = w.abs().reshape(self.cout, -1).amax(1).double()
+            e = torch.where(rmax > 0, -torch.floor(torch.log2(torch.where(rmax > 0, rmax, torch.ones_like(rmax)))),
+                            torch.zeros_like(rmax)).clamp(-100, 100)
+            row_scale = torch.pow(2.0, e).float().view(-1, 1, 1, 1, 1)
+            self.wscale = torch.pow(2.0, -e).float().contiguous()
+        else:
+            row_scale = 2.0 ** self.wexp
         ws = torch.zeros((coutp, cinp, self.kd, self.k, self.k), device=w.device, dtype=torch.float32)
-        ws[:self.cout, :self.cin] = w.permute(0, 1, 4, 2, 3) * (2.0 ** self.wexp)
+        ws[:self.cout, :self.cin] = w.permute(0, 1, 4, 2, 3) * row_scale
         # [tap = (kd, kh, kw)][cin chunk][cout][32]
         ws = ws.permute(2, 3, 4, 1, 0).reshape(self.kd * self.k * self.k, cinp // 32, 32, coutp) \
             .permute(0, 1, 3, 2).contiguous()
         hi = ws.half()
         lo = (ws - hi.float()).half()
         self.whi, self.wlo = hi.contiguous(), lo.contiguous()
+        self._sb = {}
+
+    def scale_bias(self, bias: Tensor = None) -> Tensor:
+        """(2^-wexp[co], bias[co]) pairs, 2*Cout floats, for the halo kernels' epilogue (cached
+        per bias tensor and version, so a captured graph keeps reading one stable buffer)."""
+        key = None if bias is None else (bias.data_ptr(), bias._version)
+        hit = self._sb.get(key)
+        if hit is None:
+            b = torch.zeros_like(self.wscale) if bias is None else bias.detach().float().reshape(-1)
+            assert b.numel() == self.cout, f"bias of {b.numel()} for {self.cout} output channels"
+            hit = self._sb[key] = (torch.stack([self.wscale, b], 1).contiguous(), bias)
+        return hit[0]
 
 
 def _segments(segs):
@@ -363,7 +386,7 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
     ws = _split_workspace(x.device, stream, 8 * B * pk.cout * D * H * W)
     cfg, nsplit = _tuned(pk.k, pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
     _lib.check(_lib.load().fsmi_conv3d_halo_x3(
-        _p(x), Cin, _p(pk.whi), _p(pk.wlo), pk.wexp, _p(bias) if bias is not None else None,
+        _p(x), Cin, _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
         _p(res) if res is not None else None, _p(out), B, pk.cout, D, H, W, pk.kd, pk.k, _ACT3D[act],
         1 if res_pre else 0, cfg, nsplit, _p(ws), ws.numel(), stream), "conv3d")
     return out
@@ -401,7 +424,7 @@ def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Te
     ws = _split_workspace(t0.device, stream, 8 * B * pk.cout * H * W)
     cfg, nsplit = _tuned(pk.k, 1, cin, pk.cout, B, 1, H, W, cfg, nsplit)
     _lib.check(_lib.load().fsmi_conv2d_halo_x3_gate(
-        pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, _p(bias), m, _p(h), _p(z),
+        pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)), m, _p(h), _p(z),
         _p(att) if att is not None else None, _p(rh) if rh is not None else None, Hd,
         _p(out) if out is not None else None, out.shape[1] if out is not None else 0, 0, B, pk.cout, pk.k, H, W,
         cfg, nsplit, _p(ws), ws.numel(), stream), "conv2d_gate")
@@ -433,9 +456,16 @@ def _tuned(ks, kd, cin, cout, B, D, H, W, cfg, nsplit):
             with open(_TUNE_PATH) as f:
                 _TUNE = json.load(f).get("entries", {})
     e = _TUNE.get(key)
-    if e is None:
-        return cfg, nsplit
-    return (e["cfg"] if cfg < 0 else cfg), (e["nsplit"] if nsplit < 0 else nsplit)
+    if e is not None:
+        cfg, nsplit = (e["cfg"] if cfg < 0 else cfg), (e["nsplit"] if nsplit < 0 else nsplit)
+    if _SPLIT_MAXPIX and kd == 1 and D == 1 and H * W <= _SPLIT_MAXPIX:
+        nsplit = 1
+    return cfg, nsplit
+
+
+# A/B knob: no split-K for 2D maps of at most this many pixels (the 1/8 and 1/16 GRU levels run on
+# a side stream beside gru04, so the chip is already busy and split-K only adds the reduce pass)
+_SPLIT_MAXPIX = int(os.environ.get("FSMI_SPLIT_MAXPIX", "0"))
 
 
 _SPLIT_WS = {}
@@ -492,9 +522,9 @@ def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=N
         # auto split-K is capped at 8; the workspace covers that for this output
         ws = _split_workspace(t0.device, common[-1], 8 * B * pk.cout * H * W)
         tcfg, nsplit = _tuned(pk.k, 1, cin, pk.cout, B, 1, H, W, cfg, nsplit)
-        hc = common[:9] + (pk.k,) + common[11:-2] + (tcfg, nsplit, _p(ws), ws.numel(), common[-1])
-        _lib.check(lib.fsmi_conv2d_halo_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, *hc),
-                   "conv2d_halo_x3")
+        hc = common[1:9] + (pk.k,) + common[11:-2] + (tcfg, nsplit, _p(ws), ws.numel(), common[-1])
+        _lib.check(lib.fsmi_conv2d_halo_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo),
+                                           _p(pk.scale_bias(bias)), *hc), "conv2d_halo_x3")
     del keep
     return out
 

@@ -159,14 +159,21 @@ int fsmi_conv2d(const float* const* seg_ptr, const int* seg_ch, const int* seg_c
  * x = hi + lo (two fp16), product = hi*hi + hi*lo + lo*hi accumulated in fp32
  * (~22-bit operands, ~5x the fp32-MFMA rate).  whi/wlo: _Float16 weights packed
  * [KH*KW][Cin32/32][Cout32][32] (Cin32/Cout32 = Cin/Cout rounded up to 32, zero
- * padded), pre-multiplied by 2^wexp; the epilogue multiplies by 2^-wexp. */
+ * padded), pre-multiplied by 2^wexp; the epilogue multiplies by 2^-wexp.  A/B and test
+ * kernel (the product path runs fsmi_conv2d_halo_x3): one weight exponent per tensor and no
+ * activation scaling, so it needs |x| < 65504 and keeps ~22 bits only for |x| >~ 0.1. */
 int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
                    const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
                    const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
                    int KH, int KW, int H, int W, int act, float alpha, int cfg, void* stream);
 
-/* Halo-tiled variant of fsmi_conv2d_x3 (same weights, same epilogue) for
- * square KS in {1, 3}: a block stages a (rows+2)x34 input halo once per
+/* Halo-tiled variant of fsmi_conv2d_x3 (same packed layout, same epilogue) for
+ * square KS in {1, 3}.  Range-safe split: each output channel's weights are packed
+ * x 2^wexp[co] (its max |w| in [1, 2)); scale_bias (2*Cout floats, device, 8-B
+ * aligned) holds the pairs (2^-wexp[co], bias[co]) the epilogue applies as
+ * conv * scale + bias; activations get a block exponent per 32-channel chunk in the
+ * kernel (conv_halo.h, chunk_exp), so neither overflows fp16 nor loses its low
+ * half to fp16 subnormals.  A block stages a (rows+2)x34 input halo once per
  * 32-channel chunk and runs all taps from LDS.  Inner segments must hold a
  * multiple of 8 channels.  cfg 0: 64 couts x 8x32 px, 1: 128 couts x 4x32 px
  * (weights staged per tap through LDS); 2 / 3: the same tiles with each wave's
@@ -186,7 +193,7 @@ int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* se
 int fsmi_debug_conv_timestamps(unsigned long long* buf);
 
 int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
-                        const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
+                        const void* whi, const void* wlo, const float* scale_bias, const float* gamma,
                         const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
                         int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
                         long long ws_floats, void* stream);
@@ -200,7 +207,7 @@ int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_ch, const in
  *   mode 2 (large GRU convq):            out[:, co0:] += ((1-z)h + z tanh(conv)) * (1-att).
  * conv includes the bias.  Other arguments as fsmi_conv2d_halo_x3. */
 int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
-                             const void* whi, const void* wlo, int wexp, const float* bias, int mode,
+                             const void* whi, const void* wlo, const float* scale_bias, int mode,
                              const float* h, float* z, const float* att, float* rh, int Hd, float* out,
                              int out_ctot, int co0, int B, int Cout, int KS, int H, int W, int cfg, int nsplit,
                              float* ws, long long ws_floats, void* stream);
@@ -215,7 +222,7 @@ int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* seg_ch, con
  * BatchNorm shift.  out = act(conv + bias) + res, or with res_pre
  * act(conv + bias + res); act 0 none, 1 ReLU, 6 LeakyReLU(0.01).
  * cfg as fsmi_conv2d_halo_x3 plus 6: 32 couts x 8x32 px, 7: 32 x 4x32. */
-int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wlo, int wexp, const float* bias,
+int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wlo, const float* scale_bias,
                         const float* res, float* out, int B, int Cout, int D, int H, int W, int KD, int KS,
                         int act, int res_pre, int cfg, int nsplit, float* ws, long long ws_floats, void* stream);
 

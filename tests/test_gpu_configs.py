@@ -146,3 +146,68 @@ def test_autocast_keeps_hip_convs(lib):
     d = float((outs[True] - outs[False]).abs().max())
     record("autocast_vs_fp32", d)
     assert bool(torch.isfinite(outs[True]).all()) and d < 0.5, d
+
+
+def _rescale_activations_(m, c_big=1e4, c_small=1e-4):
+    """Function-preserving rescale: for layer pairs joined by a positively homogeneous activation
+    (ReLU / LeakyReLU), multiply the producer (weight and bias, or its BatchNorm affine) by c and
+    the consumer's weights by 1/c (pairs where the producer is the consumer's whole input, so each
+    consumer row scales uniformly).  The network computes the same function in exact arithmetic,
+    but the activations between the pair -- the inputs of the split-precision convs -- now sit c
+    times higher or lower: ~1e4-1e5 (past fp16's 65504) and ~1e-4-1e-5 (fp16 subnormal).  (A naive 'checkpoint-like' random rescale of every layer makes the 32-step loop
+    chaotic: the fp32 CPU oracle then differs from itself in fp64 by 12 px, so no fp32
+    implementation could be held to 1e-3 px on it.)"""
+    ub = m.update_block
+    with torch.no_grad():
+        def pair(prod, cons_w, c, cols=None):
+            prod.weight.mul_(c)
+            if prod.bias is not None:
+                prod.bias.mul_(c)
+            if cols is None:
+                cons_w.div_(c)
+            else:
+                cons_w[:, cols].div_(c)
+        enc = ub.encoder
+        pair(enc.convc1, enc.convc2.weight, c_big)                       # 1044 -> 256 -> 256
+        pair(enc.convd1, enc.convd2.weight, c_small)                     # 1 -> 64 -> 64
+        pair(ub.mask[0], ub.mask[2].weight, c_big)
+        for name, c in (("gru04", c_big), ("gru08", c_small), ("gru16", c_big)):
+            gru = getattr(ub, name)                                      # hx = relu(conv1(.)) -> convz / convr
+            gru.conv1[0].weight.mul_(c)
+            gru.conv1[0].bias.mul_(c)
+            for rg in (gru.small_gru, gru.large_gru):
+                rg.convz.weight.div_(c)
+                rg.convr.weight.div_(c)
+        for blk, c in ((m.corr_stem[2], c_big), (m.corr_stem[3], c_small), (m.classifier[1], c_big)):
+            blk.bn1.weight.mul_(c)                                       # relu(bn1(conv1 x)) -> conv2
+            blk.bn1.bias.mul_(c)
+            blk.conv2.weight.div_(c)
+    return m
+
+
+def test_e2e_activation_range_vs_oracle(lib):
+    """cfg1 geometry (320x256, D64, 8 iterations, L=4) with the activations between homogeneous
+    layer pairs moved to ~1e4 and ~1e-4 (function-preserving, _rescale_activations_): the HIP path
+    matches the oracle on the rescaled net AND the unscaled net's result (the range-safe split
+    leaves nothing to the data's magnitude)."""
+    H, W, md, iters = 256, 320, 64, 8
+    args = synth.make_args(max_disp=md, corr_levels=4, vit_size="vits")
+    fl, fr, vf = synth.backbone_features(1, H, W, "vits", shift_px=6)
+    left, right = synth.stereo_images(1, H, W)
+    outs = {}
+    for scaled in (False, True):
+        m = _model(args)
+        if scaled:
+            _rescale_activations_(m)
+        m.feature.set_features([g(a) for a in fl], [g(a) for a in fr], g(vf))
+        with torch.no_grad():
+            outs[scaled] = m(g(left), g(right), iters=iters, test_mode=True).cpu()
+    with torch.no_grad():
+        ref = oracle.oracle_forward(_params(m), args, t(left), t(right), [t(a) for a in fl], [t(a) for a in fr],
+                                    t(vf), iters=iters)
+    assert bool(torch.isfinite(outs[True]).all())
+    d = float((outs[True] - ref).abs().max())
+    d0 = float((outs[True] - outs[False]).abs().max())
+    record("e2e_activation_range_vs_oracle", d)
+    record("e2e_activation_range_vs_unscaled", d0)
+    assert d < 1e-3 and d0 < 1e-3, (d, d0)

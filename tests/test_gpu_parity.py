@@ -198,17 +198,59 @@ def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
 
 
-@pytest.mark.gpu
-def test_conv3d_rejects_2d_only_tiles(ops_mod):
-    """cfg 8 / 9 are 2D-only tiles: a volume conv asking for them gets an error, not a launch."""
-    x = torch.zeros(1, 8, 4, 6, 8, device=DEV)
-    pk = ops_mod.PackedConv(torch.zeros(32, 8, 3, 3, 3, device=DEV), mode="halo")
-    for cfg in (8, 9):
-        with pytest.raises(RuntimeError):
-            ops_mod.conv3d(x, pk, cfg=cfg, nsplit=1)
+@pytest.mark.parametrize("scale", [3e5, 1e3, 1e-4, 1e-7])
+@pytest.mark.parametrize("cfg", [-1, 1, 3, 4, 9])
+@pytest.mark.parametrize("k", [1, 3])
+def test_conv2d_halo_range(ops_mod, scale, cfg, k):
+    """Range-safe split (conv_halo.h, chunk_exp): activations far outside fp16's range -- |x| up to
+    ~1e6 (> 65504: fp16 hi halves would overflow) and down to ~1e-7 (hi and lo subnormal) -- with
+    one input segment 1e-4x the other inside the same 32-channel chunk.  Error relative to the
+    output's magnitude stays at the 22-bit split level (vs fp64 torch), with and without split-K."""
+    import torch.nn.functional as F
+    B, H, W = 1, 12, 40
+    a_ = synth.normal(291, (B, 16, H, W)) * scale
+    c_ = synth.normal(292, (B, 40, H, W)) * (scale * 1e-4)
+    w = synth.normal(293, (64, 45, k, k), 0.2)
+    segs, x = [g(a_), (g(c_), 5, 29)], torch.cat([t(a_), t(c_[:, 5:34])], 1)
+    ref = F.conv2d(x.double(), t(w).double(), padding=k // 2)
+    for nsplit in (1, 2):
+        out = ops_mod.conv2d(segs, ops_mod.PackedConv(g(w), mode="halo"), cfg=cfg, nsplit=nsplit)
+        assert bool(torch.isfinite(out).all())
+        err = float((out.double().cpu() - ref).abs().max() / ref.abs().max())
+        assert err < 3e-6, (nsplit, err)
 
 
-@pytest.mark.parametrize("cfg", [-1, 5, 6, 7])
+@pytest.mark.parametrize("k", [1, 3])
+def test_conv2d_halo_cout_scales(ops_mod, k):
+    """Output channels whose weights differ by up to 1e12 in scale (BatchNorm folding spreads
+    gamma / sqrt(var) over decades): each row packs with its own exponent (wscale[co]), so every
+    output channel keeps the split's ~22 bits relative to its own magnitude (vs fp64 torch)."""
+    import torch.nn.functional as F
+    B, H, W, cin, cout = 1, 12, 40, 45, 64
+    x = synth.normal(391, (B, cin, H, W))
+    w = synth.normal(393, (cout, cin, k, k), 0.2) * (10.0 ** np.linspace(-6, 6, cout)).reshape(-1, 1, 1, 1)
+    w = w.astype(np.float32)
+    out = ops_mod.conv2d([g(x)], ops_mod.PackedConv(g(w), mode="halo"), nsplit=1).double().cpu()
+    ref = F.conv2d(t(x).double(), t(w).double(), padding=k // 2)
+    rel = ((out - ref).abs().amax((0, 2, 3)) / ref.abs().amax((0, 2, 3))).max()
+    assert float(rel) < 3e-6, float(rel)
+
+
+@pytest.mark.parametrize("scale", [1e5, 1e-6])
+@pytest.mark.parametrize("cfg", [-1, 6, 8, 9])
+def test_conv3d_halo_range(ops_mod, scale, cfg):
+    """The same range guarantee on NCDHW volumes (3^3 conv, chunks span kd planes)."""
+    import torch.nn.functional as F
+    x = synth.normal(591, (1, 28, 5, 9, 37)) * scale
+    w = synth.normal(592, (28, 28, 3, 3, 3), 0.15)
+    out = ops_mod.conv3d(g(x), ops_mod.PackedConv(g(w), mode="halo"), cfg=cfg)
+    ref = F.conv3d(t(x).double(), t(w).double(), padding=1)
+    assert bool(torch.isfinite(out).all())
+    err = float((out.double().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 3e-6, err
+
+
+@pytest.mark.parametrize("cfg", [-1, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("kern,cin,cout,D,act,res", [((3, 3, 3), 28, 28, 7, "leaky", None),
                                                      ((1, 3, 3), 28, 28, 5, "relu", None),
                                                      ((17, 1, 1), 28, 28, 20, "relu", None),
@@ -218,7 +260,9 @@ def test_conv3d_rejects_2d_only_tiles(ops_mod):
 def test_conv3d_halo_vs_torch(ops_mod, kern, cin, cout, D, act, res, cfg):
     """Stride-1 Conv3d on the halo kernel (sum over kd of 2D planes): 3^3, axial (1,3,3) and
     (17,1,1), 1^3 with a residual, the ResNet tail act(conv + res), ragged channels / tiles,
-    auto split-K; vs fp64 torch.  2e-5 abs + 1e-5 rel as the 2D halo conv."""
+    auto split-K, every tile incl. the 128x8 / 256x4 register tiles (cfg 8 / 9: legal on volumes
+    since the kernel's lambdas are force-inlined); vs fp64 torch.  2e-5 abs + 1e-5 rel
+    as the 2D halo conv."""
     import torch.nn.functional as F
     B, H, W = 1, 9, 37
     x = synth.normal(501, (B, cin, D, H, W))
