@@ -31,10 +31,11 @@
 #ifndef FSMI_HALO_RANGE
 #define FSMI_HALO_RANGE 1                            // 0: A/B build without the block exponent
 #endif
-// the wreg kernel's lambdas: forced inline only for the 128 x 8 x 32 volume tile, which clang
-// otherwise outlines into a real call; elsewhere the inliner's own order schedules better
+// the wreg kernel's lambdas are forced inline: left to the inliner's cost model, clang outlines
+// the 128 x 8 x 32 volume tile's `segment` into a real call (captures passed through the stack,
+// 464 B of scratch) -- the build that faulted in round 1.  Measured neutral elsewhere.
 #ifndef FSMI_HALO_FORCE_INLINE
-#define FSMI_HALO_FORCE_INLINE 0
+#define FSMI_HALO_FORCE_INLINE 1
 #endif
 #if FSMI_HALO_FORCE_INLINE
 #define FSMI_HALO_INL __attribute__((always_inline))
