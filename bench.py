@@ -212,6 +212,7 @@ def main():
     cb_ck_ms, cb_ck_n = ops.timer_query_clock("comb")
     cv_flops = ops.conv_flops()
     assert torch.isfinite(out).all()
+    range_overflow = ops.range_overflowed(reset=True)   # sticky over every forward of this run
     # roofline durations, each the live measurement that agrees with rocprof's per-launch average
     # (profiles/*kernel_stats.csv): a single event-bracketed launch also holds ~5 us of
     # event-record latency (`avg_us_events`, kept for reference).
@@ -259,6 +260,7 @@ def main():
         "dtype": ("f32 (3xfp16 split MFMA convs; library convs fp16 under autocast)" if a.mixed_precision
                   else "f32 (3xfp16 split MFMA)"),
         "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
+        "range_overflow": range_overflow,
         "config": {"workload": f"{a.config}: {W}x{H}, max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",
                    "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,

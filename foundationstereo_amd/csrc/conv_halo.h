@@ -28,9 +28,23 @@
 
 #include "fsmi_common.h"
 
+// activation range of the split.  Default (FSMI_HALO_RANGE 1):
+//   * 2D maps (mode 2): a block exponent fixed by the block's first 32-channel chunk with 8 bits
+//     of headroom, so every later chunk up to 2^9 x larger still fits fp16; a value beyond that
+//     sets the range flag (fsmi_range_status -> RangeError), never a silent inf.  Callers put the
+//     largest-magnitude input segment first where they know it (update.py: the motion encoder's
+//     disparity features ahead of its correlation features).
+//   * NCDHW volumes (mode 1): the exact block max of every chunk with accumulator rescaling --
+//     a block's first chunk there is one depth plane, and planes differ by far more than 2^9
+//     (the bias-only w < d region of the cost volume).
+// Measured end to end (cfg2): mode 2 costs ~3 % against no scaling, mode 1 on every conv ~7 %;
+// volumes are ~10 % of the conv time.  FSMI_HALO_RANGE=0 builds an A/B variant without either
+// (fp16 range: |x| < 65504, 22 bits only for |x| >~ 0.1); 2 / 3 force mode 2 / 3 everywhere.
 #ifndef FSMI_HALO_RANGE
-#define FSMI_HALO_RANGE 1                            // 0: A/B build without the block exponent
+#define FSMI_HALO_RANGE 1
 #endif
+template <bool D3>
+constexpr int range_mode() { return FSMI_HALO_RANGE == 1 ? (D3 ? 1 : 2) : FSMI_HALO_RANGE; }
 // the wreg kernel's lambdas are forced inline: left to the inliner's cost model, clang outlines
 // the 128 x 8 x 32 volume tile's `segment` into a real call (captures passed through the stack,
 // 464 B of scratch) -- the build that faulted in round 1.  Measured neutral elsewhere.
@@ -83,6 +97,7 @@ struct HaloArgs {
   const float* gatt;               // att
   float* grh;                      // sigmoid(r_pre) * h, written by act 3
   int gHd;
+  int* ovf;                        // range flag (host-mapped; set to 1 when a scaled value overflows fp16)
 };
 
 // Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
@@ -319,14 +334,23 @@ struct HaloStage {
     return m;
   }
 
-  // split x * 2^s (scale = 2^s, the block's chunk exponent) into fp16 hi + lo
-  __device__ __forceinline__ void store(_Float16 (*Xh)[HROW], _Float16 (*Xl)[HROW], int tid, float scale) const {
+  // split x * 2^s (scale = 2^s, the block exponent) into fp16 hi + lo; ovf |= an x whose scaled
+  // value leaves fp16's range
+  template <int RMODE>
+  __device__ __forceinline__ void store(_Float16 (*Xh)[HROW], _Float16 (*Xl)[HROW], int tid, float scale,
+                                        bool& ovf) const {
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u) {
       const int task = tid + 256 * u;
       if (X_TASKS % 256 == 0 || task < X_TASKS) {
         const int hp = task % NHP, g = task / NHP;
         const f32x8 x = xv[u] * scale;
+        if constexpr (RMODE == 2) {               // largest scaled |x| of the task, one compare after
+          float m = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(x[j]));
+          ovf |= m >= 65504.f;                    // (an inf input flags too; NaN is ignored by fmax)
+        }
         const half8 hi = __builtin_convertvector(x, half8);
         const half8 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x8), half8);
         *reinterpret_cast<half8*>(&Xh[hp][g * 8]) = hi;
@@ -369,11 +393,37 @@ __device__ __forceinline__ float exp2i(int e) {     // 2^e for e in [-126, 127],
   return __uint_as_float(static_cast<unsigned>(e + 127) << 23);
 }
 
-// target exponent for a chunk whose largest |x| is m (kNoExp when m == 0)
+// target exponent for a chunk whose largest |x| is m (kNoExp when m == 0): max * 2^s in
+// [2^(14-headroom), 2^(15-headroom))
+template <int HEADROOM = 0>
 __device__ __forceinline__ int chunk_exp(float m) {
   if (!(m > 0.f)) return kNoExp;
   const int e = static_cast<int>((__float_as_uint(m) >> 23) & 0xff) - 127;   // floor(log2 m); m < 2^-126 -> -127
-  return min(max(14 - e, -126), 126);
+  return min(max(14 - HEADROOM - e, -126), 126);
+}
+
+// range mode 2: the block's first chunk fixes its exponent with 8 bits of headroom, so later
+// chunks up to 2^9 x larger still fit fp16; a value beyond that raises the range flag instead
+// (fsmi_range_status) -- no per-chunk reduction and no accumulator rescale in the main loop.
+constexpr int kRangeHeadroom = 8;
+
+__device__ __forceinline__ void flag_overflow(const HaloArgs& a, bool ovf) {
+  if (ovf && a.ovf) *a.ovf = 1;    // vector store from the lanes that saw one (same value, benign race)
+}
+
+constexpr int kHeadroom3 = 4;
+constexpr int kHeadroom1 = 4;       // mode 1: exponent re-aimed 4 bits below a chunk's fit
+
+// mode 3: does any lane's chunk value overflow fp16 at scale 2^sx?  One flag word per wave.
+__device__ __forceinline__ void range3_check(int* rflag, float local_max, int sx, int lane, int wave) {
+  const bool need = local_max * exp2i(sx == kNoExp ? 0 : sx) >= 32768.f;
+  const unsigned long long any = __builtin_amdgcn_ballot_w64(need);
+  if (lane == 0) rflag[wave] = any != 0ull;
+}
+
+__device__ __forceinline__ bool range3_any(const int* rflag) {
+  const int4 f = *reinterpret_cast<const int4*>(rflag);
+  return (f.x | f.y | f.z | f.w) != 0;
 }
 
 __device__ __forceinline__ float red4_max(const float* red) {
@@ -502,11 +552,13 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   constexpr int W_PER_T = W_PIECES / 256;
   static_assert(W_PIECES % 256 == 0, "weight pieces must tile the block");
   using HS = HaloStage<KS, TR>;
+  constexpr int RM = range_mode<D3>();
   __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
   __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
   __shared__ __attribute__((aligned(16))) _Float16 Wh[2][BM][HROW];
   __shared__ __attribute__((aligned(16))) _Float16 Wl[2][BM][HROW];
   __shared__ __attribute__((aligned(16))) float red[4];   // per-wave chunk max |x| (block exponent)
+  __shared__ __attribute__((aligned(16))) int rflag[4];   // per-wave 'chunk overflows the exponent' (mode 3)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -573,21 +625,52 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
   else hs.load(a, tc.b, cc_begin);
   int sx = kNoExp;                 // block exponent of the split (see chunk_exp)
+  bool ovf = false;
   for (int cc = cc_begin; cc < cc_end; ++cc) {
-    if constexpr (FSMI_HALO_RANGE) {
+    if constexpr (RM == 3) {
+      const float lm = hs.absmax();
+      if (cc == cc_begin) {
+        const float m = wave_max(lm);
+        if (lane == 0) red[wave] = m;
+      } else {
+        range3_check(rflag, lm, sx, lane, wave);
+      }
+    } else if (RM == 1 || (RM == 2 && cc == cc_begin)) {
       const float m = wave_max(hs.absmax());
       if (lane == 0) red[wave] = m;           // m is wave-uniform (SGPR)
     }
     __syncthreads();               // every wave is done with the previous chunk's halo; maxima visible
-    if constexpr (FSMI_HALO_RANGE) {
-      const int se = __builtin_amdgcn_readfirstlane(
-          chunk_exp(red4_max(red)));     // block-uniform
-      if (se < sx) {
+    if constexpr (RM == 3) {
+      if (cc == cc_begin) {
+        const float bm = red4_max(red);
+        ovf |= !(bm <= 3.4e38f);
+        sx = bm > 0.f ? __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom3>(bm)) : 0;
+      } else if (__builtin_amdgcn_readfirstlane(range3_any(rflag))) {   // rare: beyond the headroom
+        const float m = wave_max(hs.absmax());
+        if (lane == 0) red[wave] = m;
+        __syncthreads();
+        const float bm = red4_max(red);
+        ovf |= !(bm <= 3.4e38f);
+        const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom3>(bm));
+        if (se < sx) {
+          rescale_acc<TM, TN>(acc, exp2i(se - sx));
+          sx = se;
+        }
+      }
+    } else if constexpr (RM == 1) {
+      const float bm = red4_max(red);
+      ovf |= !(bm <= 3.4e38f);                  // an inf input (NaN is ignored by the max)
+      // rescale only when the chunk does not fit the current exponent; then re-aim with headroom
+      // so that the chunks after it rarely trigger another rescale
+      if (__builtin_amdgcn_readfirstlane(chunk_exp(bm)) < sx) {
+        const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom1>(bm));     // block-uniform
         if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
         sx = se;
       }
+    } else if constexpr (RM == 2) {
+      if (cc == cc_begin) sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
     }
-    hs.store(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx));
+    hs.template store<RM>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
     if (cc + 1 < cc_end) {
       if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
       else hs.load(a, tc.b, cc + 1);
@@ -620,6 +703,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
       }
     }
   }
+  flag_overflow(a, ovf);
   conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1);
 }
 
@@ -631,9 +715,11 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
   using HS = HaloStage<KS, TR>;
+  constexpr int RM = range_mode<D3>();
   __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
   __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
   __shared__ __attribute__((aligned(16))) float red[4];   // per-wave chunk max |x| (block exponent)
+  __shared__ __attribute__((aligned(16))) int rflag[4];   // per-wave 'chunk overflows the exponent' (mode 3)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -713,22 +799,52 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
       }
     };
     int sx = kNoExp;               // block exponent of the segment (see chunk_exp)
+    bool ovf = false;
     auto stage = [&](int cc) FSMI_HALO_INL {
-      if constexpr (FSMI_HALO_RANGE) {
+      if constexpr (RM == 3) {
+        const float lm = hs.absmax();
+        if (cc == cc_begin) {
+          const float m = wave_max(lm);
+          if (lane == 0) red[wave] = m;
+        } else {
+          range3_check(rflag, lm, sx, lane, wave);
+        }
+      } else if (RM == 1 || (RM == 2 && cc == cc_begin)) {
         const float m = wave_max(hs.absmax());
-        if (lane == 0) red[wave] = m;
+        if (lane == 0) red[wave] = m;           // m is wave-uniform (SGPR)
       }
       __syncthreads();             // every wave is done with the previous chunk's halo; maxima visible
       if (tsb && tid == 0 && cc - cc_begin < 36) tsb[1 + cc - cc_begin] = wall_clock64();
-      if constexpr (FSMI_HALO_RANGE) {
-        const int se = __builtin_amdgcn_readfirstlane(
-            chunk_exp(red4_max(red)));   // block-uniform
-        if (se < sx) {
+      if constexpr (RM == 3) {
+        if (cc == cc_begin) {
+          const float bm = red4_max(red);
+          ovf |= !(bm <= 3.4e38f);
+          sx = bm > 0.f ? __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom3>(bm)) : 0;
+        } else if (__builtin_amdgcn_readfirstlane(range3_any(rflag))) {   // rare: beyond the headroom
+          const float m = wave_max(hs.absmax());
+          if (lane == 0) red[wave] = m;
+          __syncthreads();
+          const float bm = red4_max(red);
+          ovf |= !(bm <= 3.4e38f);
+          const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom3>(bm));
+          if (se < sx) {
+            rescale_acc<TM, TN>(acc, exp2i(se - sx));
+            sx = se;
+          }
+        }
+      } else if constexpr (RM == 1) {
+        const float bm = red4_max(red);
+        ovf |= !(bm <= 3.4e38f);                // an inf input (NaN is ignored by the max)
+        // rescale only when the chunk does not fit the current exponent; then re-aim with headroom
+        if (__builtin_amdgcn_readfirstlane(chunk_exp(bm)) < sx) {
+          const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom1>(bm));   // block-uniform
           if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
           sx = se;
         }
+      } else if constexpr (RM == 2) {
+        if (cc == cc_begin) sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
       }
-      hs.store(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx));
+      hs.template store<RM>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
       if (cc + 1 < cc_end && !(a.dbg & 2)) {
         if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
         else hs.load(a, tc.b, cc + 1);
@@ -751,6 +867,7 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
       chunk(std::integral_constant<int, 0>(), cc);
     }
     if (tsb && tid == 0) tsb[37] = wall_clock64();
+    flag_overflow(a, ovf);
     conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, partial);
     if (tsb && tid == 0) {
       tsb[38] = wall_clock64();

@@ -158,6 +158,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
                  "%s: split-K %d needs %lld workspace floats", what, a.nsplit, per_split * a.nsplit);
   a.ws = ws;
   a.ts = g_conv_ts;
+  a.ovf = range_flag_device();
   static const int conv_dbg = [] {
     const char* e = std::getenv("FSMI_CONV_DBG");
     return e ? std::atoi(e) : 0;

@@ -50,6 +50,12 @@ unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves)
 // amortises the event-record latency a single bracketed launch carries.
 void set_replay(int kernel, hipStream_t stream, std::function<void()> fn);
 
+// Range flag of the split-precision convs (runtime.hip): one host-mapped int (pinned host memory
+// the GPU writes through its device alias), allocated on first use; kernels store 1 into it when
+// a scaled activation left fp16's range.  Read / reset by fsmi_range_status.  nullptr if the
+// allocation failed (the kernels then skip the flag).
+int* range_flag_device();
+
 __device__ __forceinline__ long long clock_wave_id() {
   const long long blk = blockIdx.x + static_cast<long long>(gridDim.x) * (blockIdx.y + static_cast<long long>(gridDim.y) * blockIdx.z);
   return blk * ((blockDim.x * blockDim.y * blockDim.z + 63) / 64) + (threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z)) / 64;

@@ -91,6 +91,29 @@ void set_replay(int kernel, hipStream_t stream, std::function<void()> fn) {
   g_replay_stream[kernel] = stream;
 }
 
+namespace {
+std::mutex g_range_mu;
+int* g_range_host = nullptr;
+int* g_range_dev = nullptr;
+}  // namespace
+
+int* range_flag_device() {
+  std::lock_guard<std::mutex> lk(g_range_mu);
+  if (!g_range_dev) {
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, sizeof(int), hipHostMallocMapped) != hipSuccess) return nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return nullptr;
+    }
+    g_range_host = static_cast<int*>(h);
+    *g_range_host = 0;
+    g_range_dev = static_cast<int*>(d);
+  }
+  return g_range_dev;
+}
+
 LaunchTimer::LaunchTimer(int kernel, hipStream_t stream) : stream_(stream) {
   if (!g_enabled) return;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -184,6 +207,18 @@ int fsmi_timer_replay(int kernel, int reps, double* avg_ms) {
     return static_cast<int>(e);
   }
   if (avg_ms) *avg_ms = static_cast<double>(ms) / reps;
+  return FSMI_OK;
+}
+
+int fsmi_range_status(int reset, int* overflowed) {
+  FSMI_CHECK_ARG(overflowed, "fsmi_range_status: null pointer");
+  if (!fsmi::range_flag_device()) {
+    fsmi::set_error("fsmi_range_status: host-mapped flag unavailable");
+    return FSMI_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(fsmi::g_range_mu);
+  *overflowed = __atomic_load_n(fsmi::g_range_host, __ATOMIC_ACQUIRE);
+  if (reset) __atomic_store_n(fsmi::g_range_host, 0, __ATOMIC_RELEASE);
   return FSMI_OK;
 }
 

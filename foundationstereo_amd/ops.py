@@ -394,6 +394,14 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
 
 _GATE_MODE = {"zr": 0, "blend_small": 1, "blend_large": 2}
 
+_RANGE_DEBUG = os.environ.get("FSMI_RANGE_DEBUG", "0") == "1"   # diagnostics: sync + check after each conv
+
+
+def _range_debug(what, segs):
+    if _RANGE_DEBUG and not torch.cuda.is_current_stream_capturing() and range_overflowed(reset=True):
+        desc = [(tuple(t.shape), c0, n, float(t[:, c0:c0 + n].abs().max())) for t, c0, n in segs]
+        print(f"[fsmi range] {what}: segments (shape, c0, n, max|x|) {desc}", flush=True)
+
 
 def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Tensor = None, rh: Tensor = None,
                 out: Tensor = None, nsplit: int = -1, cfg: int = -1):
@@ -428,6 +436,7 @@ def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Te
         _p(att) if att is not None else None, _p(rh) if rh is not None else None, Hd,
         _p(out) if out is not None else None, out.shape[1] if out is not None else 0, 0, B, pk.cout, pk.k, H, W,
         cfg, nsplit, _p(ws), ws.numel(), stream), "conv2d_gate")
+    _range_debug(f"conv2d_gate {mode} k{pk.k} {cin}->{pk.cout}", norm)
     del keep
 
 
@@ -525,6 +534,7 @@ def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=N
         hc = common[1:9] + (pk.k,) + common[11:-2] + (tcfg, nsplit, _p(ws), ws.numel(), common[-1])
         _lib.check(lib.fsmi_conv2d_halo_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo),
                                            _p(pk.scale_bias(bias)), *hc), "conv2d_halo_x3")
+        _range_debug(f"conv2d k{pk.k} {cin}->{pk.cout}", norm)
     del keep
     return out
 
@@ -642,6 +652,30 @@ def upsample4_add_(vol: Tensor, t: Tensor) -> Tensor:
     t = _c(t)
     _lib.check(_lib.load().fsmi_upsample4_add(_p(t), _p(vol), B, C, D, H, W, _stream(vol)), "upsample4_add_")
     return vol
+
+
+# ---------------------------------------------------------------- range guard
+
+class RangeError(_lib.FsmiError):
+    """A split-precision conv saw an activation its block exponent could not bring into fp16's
+    range (more than 2^9 x the largest value of the block's first 32-channel chunk)."""
+
+
+def range_overflowed(reset: bool = True) -> bool:
+    """Whether any halo conv overflowed since the last reset (fsmi_range_status).  Asynchronous:
+    synchronises the device first."""
+    import ctypes
+    torch.cuda.synchronize()
+    flag = ctypes.c_int(0)
+    _lib.check(_lib.load().fsmi_range_status(1 if reset else 0, ctypes.byref(flag)), "range_status")
+    return bool(flag.value)
+
+
+def check_range():
+    """Raise RangeError if a halo conv overflowed since the last check (then resets the flag)."""
+    if range_overflowed(reset=True):
+        raise RangeError("split-precision conv: an activation exceeded fp16's range after the block "
+                         "exponent (inputs spanning > 2^9 within one conv tile)")
 
 
 # ---------------------------------------------------------------- timing

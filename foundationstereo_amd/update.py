@@ -52,19 +52,24 @@ def _f32s(xs):
     return [_f32(x) for x in xs]
 
 
-def _packed(*mods):
+def _packed(*mods, cin_order=None):
     """Halo-kernel weights of one Conv2d/Linear (or several stacked along Cout),
-    cached on the first module and rebuilt when any weight/bias changes."""
+    cached on the first module and rebuilt when any weight/bias changes.  ``cin_order``: input
+    channels packed in this order (the caller passes its segments in the same order)."""
     key = tuple((id(m), m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version)
-                for m in mods)
-    hit = mods[0].__dict__.get("_fsmi_pack")
+                for m in mods) + (tuple(cin_order) if cin_order is not None else None,)
+    slot = "_fsmi_pack" if cin_order is None else "_fsmi_pack_perm"
+    hit = mods[0].__dict__.get(slot)
     if hit is None or hit[0] != key:
         with torch.no_grad():
             ws = [m.weight if m.weight.dim() == 4 else m.weight[:, :, None, None] for m in mods]
+            if cin_order is not None:
+                idx = torch.as_tensor(list(cin_order), device=ws[0].device)
+                ws = [w.index_select(1, idx) for w in ws]
             pk = ops.PackedConv(*ws, mode="halo")
             bias = torch.cat([m.bias.detach().float() for m in mods]).contiguous()
         hit = (key, pk, bias)
-        mods[0].__dict__["_fsmi_pack"] = hit
+        mods[0].__dict__[slot] = hit
     return hit[1], hit[2]
 
 
@@ -162,7 +167,11 @@ class BasicMotionEncoder(nn.Module):
         else:
             d = ops.conv2d_1in(disp, self.convd1.weight, self.convd1.bias, relu=True)   # 7x7, 1 -> 64
         d = _conv(self.convd2, [d], "relu")
-        _conv(self.conv, [c, d], "relu", out=out, co0=0)
+        # cat([cor, dsp]) with the disparity features (~disp magnitude: ~200 at cfg5) as the FIRST
+        # segment: the halo conv fixes a block's exponent from its first chunk (conv_halo.h)
+        nc, nd = c.shape[1], d.shape[1]
+        pk, b = _packed(self.conv, cin_order=tuple(range(nc, nc + nd)) + tuple(range(nc)))
+        ops.conv2d([d, c], pk, bias=b, act="relu", out=out, co0=0)
         out[:, self.conv.out_channels:].copy_(disp)
         return out
 

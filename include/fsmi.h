@@ -275,6 +275,13 @@ enum {
   FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
   FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_DWCONV, FSMI_K_RESIZE, FSMI_K_DT, FSMI_K_COUNT
 };
+/* Range guard of the split-precision convs: a block scales its activations by a power of two
+ * fixed from its first 32-channel chunk (8 bits of headroom); a later value that would still
+ * leave fp16's range sets a host-mapped flag instead of silently becoming inf.  *overflowed =
+ * the flag (1 once any conv since the last reset overflowed); reset != 0 clears it.  The flag
+ * is written asynchronously: synchronise the streams that ran the convs before reading it. */
+int fsmi_range_status(int reset, int* overflowed);
+
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
 int fsmi_timer_query(int kernel, double* total_ms, long long* count);

@@ -17,7 +17,7 @@ import pytest
 import torch
 
 import oracle
-from foundationstereo_amd import synth
+from foundationstereo_amd import ops, synth
 from tests.helpers import load_golden, t
 
 pytestmark = pytest.mark.gpu
@@ -74,8 +74,10 @@ def test_config_vs_oracle(lib, name, H, W, md, iters, vit, B):
     fl, fr, vf = synth.backbone_features(B, H, W, vit, shift_px=8)
     left, right = synth.stereo_images(B, H, W)
     m.feature.set_features([g(a) for a in fl], [g(a) for a in fr], g(vf))
+    ops.range_overflowed(reset=True)
     with torch.no_grad():
         out = m(g(left), g(right), iters=iters, test_mode=True).cpu()
+        assert not ops.range_overflowed(), "a split-precision conv left fp16's range"
         ref = oracle.oracle_forward(_params(m), args, t(left), t(right), [t(a) for a in fl], [t(a) for a in fr],
                                     t(vf), iters=iters)
     assert out.shape == (B, 1, H, W)
@@ -109,9 +111,11 @@ def test_cfg5_hierarchical_vs_oracle(lib):
     m = _model(args)
     m.feature.shift_px = 8
     left, right = synth.stereo_images(1, H, W)
+    ops.range_overflowed(reset=True)
     with torch.no_grad():
         out = m.run_hierachical(g(left), g(right), iters=iters, test_mode=True).cpu()
         assert out.shape == (1, 1, H, W) and bool(torch.isfinite(out).all())
+        assert not ops.range_overflowed(), "a split-precision conv left fp16's range"
         ref = oracle.oracle_hierarchical(_params(m), args, t(left), t(right), synth_features("vitl", 8),
                                          iters=iters)
     d = float((out - ref).abs().max())
@@ -195,6 +199,7 @@ def test_e2e_activation_range_vs_oracle(lib):
     fl, fr, vf = synth.backbone_features(1, H, W, "vits", shift_px=6)
     left, right = synth.stereo_images(1, H, W)
     outs = {}
+    ops.range_overflowed(reset=True)
     for scaled in (False, True):
         m = _model(args)
         if scaled:
@@ -205,7 +210,7 @@ def test_e2e_activation_range_vs_oracle(lib):
     with torch.no_grad():
         ref = oracle.oracle_forward(_params(m), args, t(left), t(right), [t(a) for a in fl], [t(a) for a in fr],
                                     t(vf), iters=iters)
-    assert bool(torch.isfinite(outs[True]).all())
+    assert bool(torch.isfinite(outs[True]).all()) and not ops.range_overflowed()
     d = float((outs[True] - ref).abs().max())
     d0 = float((outs[True] - outs[False]).abs().max())
     record("e2e_activation_range_vs_oracle", d)

@@ -220,6 +220,24 @@ def test_conv2d_halo_range(ops_mod, scale, cfg, k):
         assert err < 3e-6, (nsplit, err)
 
 
+def test_conv2d_halo_range_flag(ops_mod):
+    """A value more than 2^9 x the largest of its block's first 32-channel chunk cannot be brought
+    into fp16 by the block exponent: the conv raises the range flag (ops.check_range ->
+    RangeError) instead of silently returning inf; in-range calls leave it clear."""
+    B, H, W = 1, 8, 32
+    small = synth.normal(381, (B, 32, H, W)) * 1e-3          # chunk 0
+    big = synth.normal(382, (B, 32, H, W)) * 1e4             # chunk 1: 1e7 x chunk 0
+    w = synth.normal(383, (16, 64, 3, 3), 0.2)
+    pk = ops_mod.PackedConv(g(w), mode="halo")
+    ops_mod.range_overflowed(reset=True)
+    ops_mod.conv2d([g(big), g(small)], pk, nsplit=1)        # large chunk first: fine
+    ops_mod.check_range()
+    ops_mod.conv2d([g(small), g(big)], pk, nsplit=1)
+    with pytest.raises(ops_mod.RangeError):
+        ops_mod.check_range()
+    assert not ops_mod.range_overflowed()                   # check_range reset it
+
+
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv2d_halo_cout_scales(ops_mod, k):
     """Output channels whose weights differ by up to 1e12 in scale (BatchNorm folding spreads
