@@ -45,8 +45,19 @@ CONFIGS = {
     "cfg2": (480, 640, 192, 32, "vits", 1),
     "cfg3": (480, 640, 192, 32, "vitl", 4),   # batch 32 over 8 GPUs
     "cfg4": (384, 1248, 256, 32, "vitl", 1),  # batch 8 over 8 GPUs
+    "cfg5": (1024, 1536, 320, 22, "vitl", 1),  # --hiera: run_hierachical, 768x512 coarse + full pass
     "tiny": (64, 96, 32, 4, "vits", 1),
 }
+HIERA = {"cfg5"}
+
+
+def pass_sizes(config, H, W):
+    """Image sizes the forward passes of ``config`` see: the /32-padded half-size coarse pass and
+    the full pass for run_hierachical (core/foundation_stereo.py:257-274), else just (H, W)."""
+    if config not in HIERA:
+        return [(H, W)]
+    hs, ws = int(H * 0.5), int(W * 0.5)
+    return [(hs + (-hs) % 32, ws + (-ws) % 32), (H + (-H) % 32, W + (-W) % 32)]
 
 
 def lookup_bytes(B, H4, W4, Cv, L, r):
@@ -73,7 +84,7 @@ def make_model(args, device, rank):
     return m
 
 
-def cpu_baseline(args, H, W, iters, threads):
+def cpu_baseline(args, H, W, iters, threads, hiera=False):
     """Time the CPU oracle on one pair of the same workload on the host cores."""
     import oracle
     torch.set_num_threads(threads)
@@ -81,14 +92,21 @@ def cpu_baseline(args, H, W, iters, threads):
     m = FoundationStereo(args)
     synth.init_module_(m, seed=1234)
     P = {k: v.float() if v.is_floating_point() else v for k, v in m.state_dict().items()}
-    fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, shift_px=8)
     left, right = synth.stereo_images(1, H, W)
     T = oracle.StageTimer()
     t0 = time.perf_counter()
     with torch.no_grad():
-        oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
-                              [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr],
-                              torch.from_numpy(vf), iters=iters, timer=T)
+        if hiera:
+            def features(B, h, w):
+                fl, fr, vf = synth.backbone_features(B, h, w, args.vit_size, shift_px=8)
+                return [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr], torch.from_numpy(vf)
+            oracle.oracle_hierarchical(P, args, torch.from_numpy(left), torch.from_numpy(right), features,
+                                       iters=iters, timer=T)
+        else:
+            fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, shift_px=8)
+            oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
+                                  [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr],
+                                  torch.from_numpy(vf), iters=iters, timer=T)
     dt = time.perf_counter() - t0
     return dt, T.stages
 
@@ -141,12 +159,14 @@ def main():
     _lib.load()
     B = per_gpu * world
     lo, hi = fdist.shard_range(B, rank, world)
-    # this rank's backbone output, resident in HBM (seed = 0x5EED + global pair index)
-    feats = [synth.backbone_features(1, H, W, vit, seed=0x5EED + i, shift_px=8) for i in range(lo, hi)]
-    fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(device) for j in range(4)]
-    fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(device) for j in range(4)]
-    vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(device)
-    model.feature.set_features(fl, fr, vf)
+    # this rank's backbone output, resident in HBM (seed = 0x5EED + global pair index), per pass size
+    sizes = pass_sizes(a.config, H, W)
+    for (ph, pw) in sizes:
+        feats = [synth.backbone_features(1, ph, pw, vit, seed=0x5EED + i, shift_px=8) for i in range(lo, hi)]
+        fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(device) for j in range(4)]
+        fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(device) for j in range(4)]
+        vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(device)
+        model.feature.set_features(fl, fr, vf, size=(ph, pw))
     if rank == 0:
         left, right = synth.stereo_images(B, H, W)
         batch = torch.from_numpy(np.stack([left, right], 1)).to(device)
@@ -154,6 +174,8 @@ def main():
         batch = torch.empty((1, 1, 1, 1, 1), device=device).expand(B, 2, 3, H, W)
 
     def fn(lft, rgt):
+        if a.config in HIERA:
+            return model.run_hierachical(lft, rgt, iters=iters, test_mode=True)
         return model(lft, rgt, iters=iters, test_mode=True)
 
     runner = fdist.ShardedStereo(fn, rank, world)
@@ -227,12 +249,13 @@ def main():
     cb_rep = ops.timer_replay("comb", REPS) if cb_n else None
     ops.timer_enable(False)
 
-    H4, W4, D4 = H // 4, W // 4, md // 4
+    D4 = md // 4
     bl = hi - lo
-    lk_bytes = lookup_bytes(bl, H4, W4, 28, L, args.corr_radius)
-    lk_avg = lk_rep / 1e3 if lk_rep else (lk_ms / 1e3) / max(lk_n, 1)
     C = synth.feature_dims(vit)[0][0]
-    cb_bytes = build_bytes(bl, C, H4, W4, D4)
+    # algorithmic bytes per launch, averaged over the passes (one size unless hierarchical)
+    lk_bytes = sum(lookup_bytes(bl, ph // 4, pw // 4, 28, L, args.corr_radius) for ph, pw in sizes) / len(sizes)
+    cb_bytes = build_bytes(bl, C, sizes[-1][0] // 4, sizes[-1][1] // 4, D4)   # the replayed (last) launch
+    lk_avg = lk_rep / 1e3 if lk_rep else (lk_ms / 1e3) / max(lk_n, 1)
     cb_avg = cb_rep / 1e3 if cb_rep else (cb_ms / 1e3) / max(cb_n, 1)
     traffic = traffic_build = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_lookup_summary.json")
@@ -245,7 +268,7 @@ def main():
 
     pairs = a.steps * B
     res = {
-        "metric": "stereo pairs/sec (32 refinement iters)",
+        "metric": f"stereo pairs/sec ({iters} refinement iters)",
         "value": pairs / elapsed,
         "unit": "pairs/s",
         "n_gpus": world,
@@ -261,7 +284,8 @@ def main():
                   else "f32 (3xfp16 split MFMA)"),
         "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
         "range_overflow": range_overflow,
-        "config": {"workload": f"{a.config}: {W}x{H}, max_disp {md}, {iters} iters, {vit}, "
+        "config": {"workload": f"{a.config}: {W}x{H}{' hierarchical' if a.config in HIERA else ''}, "
+                               f"max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",
                    "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,
                    "corr_levels": L, "conv_engine": a.conv_engine, "hip_graph": bool(a.graph),
@@ -293,7 +317,7 @@ def main():
         # the host cores this process is given: OMP_NUM_THREADS (16 on the GPU box = its CPU share
         # per GPU; os.cpu_count() there reports the whole machine, shared with other jobs)
         threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1)
-        dt, stages = cpu_baseline(args, H, W, iters, threads)
+        dt, stages = cpu_baseline(args, H, W, iters, threads, hiera=a.config in HIERA)
         res["cpu_baseline"] = {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
                                "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
                                "sample": f"1 pair of {a.config} (all {iters} iterations) through the fp32 "

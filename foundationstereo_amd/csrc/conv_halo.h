@@ -103,7 +103,11 @@ struct HaloArgs {
 // Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
 // (D3); defined in conv_halo_k<KS>_<2d|3d>.hip.  Returns FSMI_OK or an error code.
 template <int KS, bool D3>
-int launch_cfg(int cfg, const HaloArgs& a, hipStream_t s);
+int launch_cfg(int cfg, int kg, const HaloArgs& a, hipStream_t s);
+
+// tiles with an in-block K-group (kg = 2) instantiation: the register-weight tiles that fit two
+// waves per SIMD (<= 256 VGPRs) with 512-thread blocks
+inline bool kg2_tile(int cfg) { return cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7; }
 
 }  // namespace halo
 
@@ -493,7 +497,7 @@ __device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM
 // Non-split epilogue of the block's tile with the activation fixed at compile time
 template <int ACT, int TM, int TN, bool D3>
 __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv, const TileCoord& t,
-                                         int wm, int wn, int lane) {
+                                         int wm, int wn, int lane, unsigned fown) {
   const int hsel = lane >> 5, rl = lane & 31;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -502,6 +506,7 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
     const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
+      if ((fown >> (i * TN + j)) & 1u)
       store_frag<ACT, D3>(a, acc[i][j], xinv, t.m0 + (wm * TM + i) * 32 + 4 * hsel, t.b, hw, a.out, a.sb, a.gamma,
                           a.res, a.gh, a.gz, a.gatt, a.grh);
   }
@@ -510,7 +515,8 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
 // n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
 template <int TM, int TN, bool D3>
 __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv,
-                                              const TileCoord& t, int wm, int wn, int lane, bool partial) {
+                                              const TileCoord& t, int wm, int wn, int lane, bool partial,
+                                              unsigned fown = ~0u) {
   const int hsel = lane >> 5, rl = lane & 31;
   const long long HW = a.cstride;
   if (partial) {                   // raw partial sums into ws slot t.split; a reduce applies the epilogue
@@ -521,23 +527,25 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
       const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
       float* wp = a.ws + (static_cast<size_t>(t.split) * a.B + t.b) * a.Cout * HW + hw;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        if (!((fown >> (i * TN + j)) & 1u)) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = t.m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
           if (co < a.Cout) wp[static_cast<size_t>(co) * HW] = acc[i][j][r] * xinv;   // packed units
         }
+      }
     }
     return;
   }
   switch (a.act) {                 // uniform: one specialised tile epilogue per activation
-    case 1: epi_tile<1, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
-    case 2: epi_tile<2, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
-    case 3: epi_tile<3, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
-    case 4: epi_tile<4, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
-    case 5: epi_tile<5, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
-    case 6: epi_tile<6, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
-    default: epi_tile<0, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane); break;
+    case 1: epi_tile<1, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    case 2: epi_tile<2, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    case 3: epi_tile<3, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    case 4: epi_tile<4, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    case 5: epi_tile<5, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    case 6: epi_tile<6, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    default: epi_tile<0, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
   }
 }
 
@@ -709,27 +717,36 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
 
 // ---------------------------------------------------------------- cfg 2/3: weights in registers
 
-template <int KS, int BM, int TR, int WM, bool D3>
-__global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
+// KG = 2 ("K groups"): the block runs two groups of four waves on one tile, each accumulating
+// every other (kd, channel) chunk with its own halo buffers, and sums the two halves through LDS
+// before the epilogue -- split-K inside one workgroup, with no partial sums through memory and
+// no reduce pass; each group then runs the epilogue of half of the fragments.
+template <int KS, int BM, int TR, int WM, bool D3, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
+  static_assert(KG == 1 || KG == 2, "K groups: 1 or 2");
   using HS = HaloStage<KS, TR>;
   constexpr int RM = range_mode<D3>();
-  __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
-  __shared__ __attribute__((aligned(16))) float red[4];   // per-wave chunk max |x| (block exponent)
-  __shared__ __attribute__((aligned(16))) int rflag[4];   // per-wave 'chunk overflows the exponent' (mode 3)
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[KG][HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[KG][HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) float red[KG][4];   // per-wave chunk max |x| (block exponent)
+  // K-group exchange (2 x 16 KB): the halo buffers when they are large enough, else its own
+  constexpr bool XCH_IN_HALO = sizeof(_Float16) * KG * HS::NHP * HROW >= 16 * 256 * sizeof(float);
+  __shared__ __attribute__((aligned(16))) float xch_own[(KG == 2 && !XCH_IN_HALO) ? 2 * 16 * 256 : 1];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = KG == 1 ? 0 : static_cast<int>(threadIdx.x >> 8);
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int hsel = lane >> 5, rl = lane & 31;
   const int nck = a.CinP / HKC;
   const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
   unsigned long long* tsb = a.ts ? a.ts + static_cast<size_t>(blockIdx.x) * 40 : nullptr;
-  if (tsb && tid == 0) tsb[0] = wall_clock64();
+  if (tsb && threadIdx.x == 0) tsb[0] = wall_clock64();
 
-  // one segment: chunks [cc_begin, cc_end) of tile tc; partial: raw sums into ws slot tc.split
+  // one segment: chunks [cc_begin, cc_end) of tile tc (group g: cc_begin + g, + g + KG, ...);
+  // partial: raw sums into ws slot tc.split
   auto segment = [&](const TileCoord& tc, int cc_begin, int cc_end, bool partial) FSMI_HALO_INL {
     // this lane's A-fragment rows (rows past Cout only feed outputs the epilogue drops:
     // clamped so every address is mapped, no zeroing needed)
@@ -752,6 +769,9 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
     };
     HS hs;
     hs.init(a, tid, tc.r0, tc.c0);
+    _Float16 (*gXh)[HROW] = Xh[grp];
+    _Float16 (*gXl)[HROW] = Xl[grp];
+    float* gred = red[grp];
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -761,6 +781,10 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    const int c_first = cc_begin + grp;              // this group's chunks: c_first, c_first + KG, ...
+    const int n_g = c_first < cc_end ? (cc_end - c_first + KG - 1) / KG : 0;
+    const int c_last = c_first + KG * max(n_g - 1, 0);
+
     // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
     auto chunk = [&](auto par_c, int cc) FSMI_HALO_INL {
       constexpr int P = decltype(par_c)::value;
@@ -768,9 +792,9 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
       for (int tap = 0; tap < NTAP; ++tap) {
         const bool last = tap + 1 == NTAP;
         if (((tap + P) & 1) == 0) {
-          load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+          load_wf(std::integral_constant<int, 1>(), last ? min(cc + KG, c_last) : cc, last ? 0 : tap + 1);
         } else {
-          load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, cc_end - 1) : cc, last ? 0 : tap + 1);
+          load_wf(std::integral_constant<int, 0>(), last ? min(cc + KG, c_last) : cc, last ? 0 : tap + 1);
         }
         // issue the next tap's loads before this tap's MFMAs: unfenced, the scheduler sinks them
         // below the last MFMA and reuses the current buffer's registers -- a single buffer whose
@@ -788,8 +812,8 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
-            bh[j] = *reinterpret_cast<const half8*>(&Xh[hp][16 * k + 8 * hsel]);
-            bl[j] = *reinterpret_cast<const half8*>(&Xl[hp][16 * k + 8 * hsel]);
+            bh[j] = *reinterpret_cast<const half8*>(&gXh[hp][16 * k + 8 * hsel]);
+            bl[j] = *reinterpret_cast<const half8*>(&gXl[hp][16 * k + 8 * hsel]);
           }
           mma3<TM, TN>(acc, ah, al, bh, bl);
         }
@@ -798,78 +822,97 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    int sx = kNoExp;               // block exponent of the segment (see chunk_exp)
+    int sx = kNoExp;               // block (group) exponent of the segment (see chunk_exp)
     bool ovf = false;
-    auto stage = [&](int cc) FSMI_HALO_INL {
-      if constexpr (RM == 3) {
-        const float lm = hs.absmax();
-        if (cc == cc_begin) {
-          const float m = wave_max(lm);
-          if (lane == 0) red[wave] = m;
-        } else {
-          range3_check(rflag, lm, sx, lane, wave);
-        }
-      } else if (RM == 1 || (RM == 2 && cc == cc_begin)) {
+    // q-th chunk of this group (cc = c_first + KG q); both groups run the same number of stages
+    // (barriers), a group past its last chunk idles through them
+    auto stage = [&](int q) FSMI_HALO_INL {
+      const int cc = c_first + KG * q;
+      const bool valid = q < n_g;
+      if (valid && (RM == 1 || (RM == 2 && q == 0))) {
         const float m = wave_max(hs.absmax());
-        if (lane == 0) red[wave] = m;           // m is wave-uniform (SGPR)
+        if (lane == 0) gred[wave] = m;          // m is wave-uniform (SGPR)
       }
       __syncthreads();             // every wave is done with the previous chunk's halo; maxima visible
-      if (tsb && tid == 0 && cc - cc_begin < 36) tsb[1 + cc - cc_begin] = wall_clock64();
-      if constexpr (RM == 3) {
-        if (cc == cc_begin) {
-          const float bm = red4_max(red);
-          ovf |= !(bm <= 3.4e38f);
-          sx = bm > 0.f ? __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom3>(bm)) : 0;
-        } else if (__builtin_amdgcn_readfirstlane(range3_any(rflag))) {   // rare: beyond the headroom
-          const float m = wave_max(hs.absmax());
-          if (lane == 0) red[wave] = m;
-          __syncthreads();
-          const float bm = red4_max(red);
-          ovf |= !(bm <= 3.4e38f);
-          const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom3>(bm));
-          if (se < sx) {
-            rescale_acc<TM, TN>(acc, exp2i(se - sx));
+      if (tsb && threadIdx.x == 0 && q < 36) tsb[1 + q] = wall_clock64();
+      if (valid) {
+        if constexpr (RM == 1) {
+          const float bm = red4_max(gred);
+          ovf |= !(bm <= 3.4e38f);              // an inf input (NaN is ignored by the max)
+          // rescale only when the chunk does not fit the current exponent; then re-aim with headroom
+          if (__builtin_amdgcn_readfirstlane(chunk_exp(bm)) < sx) {
+            const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom1>(bm));   // group-uniform
+            if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
             sx = se;
           }
+        } else if constexpr (RM == 2) {
+          if (q == 0) sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(gred)));
         }
-      } else if constexpr (RM == 1) {
-        const float bm = red4_max(red);
-        ovf |= !(bm <= 3.4e38f);                // an inf input (NaN is ignored by the max)
-        // rescale only when the chunk does not fit the current exponent; then re-aim with headroom
-        if (__builtin_amdgcn_readfirstlane(chunk_exp(bm)) < sx) {
-          const int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom1>(bm));   // block-uniform
-          if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
-          sx = se;
-        }
-      } else if constexpr (RM == 2) {
-        if (cc == cc_begin) sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
+        hs.template store<RM>(gXh, gXl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
+        if (cc + KG < cc_end && !(a.dbg & 2)) {
+          if constexpr (D3) hs.load(a, tc.b, (cc + KG) % nck, tc.d0 + (cc + KG) / nck - a.PDD);
+          else hs.load(a, tc.b, cc + KG);
+        }   // in flight during this chunk's taps
       }
-      hs.template store<RM>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
-      if (cc + 1 < cc_end && !(a.dbg & 2)) {
-        if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
-        else hs.load(a, tc.b, cc + 1);
-      }   // in flight during this chunk's taps
       __syncthreads();
     };
-    load_wf(std::integral_constant<int, 0>(), cc_begin, 0);
-    if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
-    else hs.load(a, tc.b, cc_begin);
+    if (n_g > 0) {
+      load_wf(std::integral_constant<int, 0>(), c_first, 0);
+      if constexpr (D3) hs.load(a, tc.b, c_first % nck, tc.d0 + c_first / nck - a.PDD);
+      else hs.load(a, tc.b, c_first);
+    }
     // chunks in pairs so every register-buffer index is static (parity 0, then 1)
-    int cc = cc_begin;
-    for (; cc + 1 < cc_end; cc += 2) {
-      stage(cc);
-      chunk(std::integral_constant<int, 0>(), cc);
-      stage(cc + 1);
-      chunk(std::integral_constant<int, 1>(), cc + 1);
+    const int n_all = (cc_end - cc_begin + KG - 1) / KG;   // stages every group runs
+    int q = 0;
+    for (; q + 1 < n_all; q += 2) {
+      stage(q);
+      if (q < n_g) chunk(std::integral_constant<int, 0>(), c_first + KG * q);
+      stage(q + 1);
+      if (q + 1 < n_g) chunk(std::integral_constant<int, 1>(), c_first + KG * (q + 1));
     }
-    if (cc < cc_end) {
-      stage(cc);
-      chunk(std::integral_constant<int, 0>(), cc);
+    if (q < n_all) {
+      stage(q);
+      if (q < n_g) chunk(std::integral_constant<int, 0>(), c_first + KG * q);
     }
-    if (tsb && tid == 0) tsb[37] = wall_clock64();
+    if (tsb && threadIdx.x == 0) tsb[37] = wall_clock64();
     flag_overflow(a, ovf);
-    conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, partial);
-    if (tsb && tid == 0) {
+    float xinv = exp2i(sx == kNoExp ? 0 : -sx);
+    unsigned fown = ~0u;
+    if constexpr (KG == 2) {
+      // the other group's half of every fragment this group finishes, through LDS (the halo
+      // buffers, free once both groups are past their last chunk): fragment f = i*TN + j is
+      // finished by group f & 1 (group 0 when there is only one), in rounds of two fragments
+      // (one per direction, 16 KB each)
+      constexpr int F = TM * TN;
+      float* xb = XCH_IN_HALO ? reinterpret_cast<float*>(&Xh[0][0][0]) : xch_own;
+      float* xbB = XCH_IN_HALO ? reinterpret_cast<float*>(&Xl[0][0][0]) : xch_own + 16 * 256;
+      fown = 0u;
+#pragma unroll
+      for (int pr = 0; pr < (F + 1) / 2; ++pr) {
+        const int f0 = 2 * pr, f1 = 2 * pr + 1;      // f0 finished by group 0, f1 by group 1
+        __syncthreads();
+        if (grp == 1) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xb[r * 256 + tid] = acc[f0 / TN][f0 % TN][r] * xinv;
+        } else if (f1 < F) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xbB[r * 256 + tid] = acc[f1 / TN][f1 % TN][r] * xinv;
+        }
+        __syncthreads();
+        if (grp == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[f0 / TN][f0 % TN][r] = acc[f0 / TN][f0 % TN][r] * xinv + xb[r * 256 + tid];
+          fown |= 1u << f0;
+        } else if (f1 < F) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[f1 / TN][f1 % TN][r] = acc[f1 / TN][f1 % TN][r] * xinv + xbB[r * 256 + tid];
+          fown |= 1u << f1;
+        }
+      }
+      xinv = 1.f;
+    }
+    conv_epilogue<TM, TN, D3>(a, acc, xinv, tc, wm, wn, lane, partial, fown);
+    if (tsb && threadIdx.x == 0) {
       tsb[38] = wall_clock64();
       tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
     }
@@ -880,10 +923,11 @@ __global__ __launch_bounds__(256) void conv_halo_wreg_kernel(HaloArgs a) {
   segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
 }
 
-template <int KS, int BM, int TR, int WM, bool WREG, bool D3>
+template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1>
 void launch_tile(const HaloArgs& a, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
-  if constexpr (WREG) hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);
+  if constexpr (WREG)
+    hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3, KG>), dim3(grid), dim3(256 * KG), 0, s, a);
   else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);
 }
 
@@ -895,7 +939,17 @@ void launch_tile(const HaloArgs& a, hipStream_t s) {
   namespace fsmi {                                                                          \
   namespace halo {                                                                          \
   template <>                                                                               \
-  int launch_cfg<KS, D3>(int cfg, const HaloArgs& a, hipStream_t s) {                      \
+  int launch_cfg<KS, D3>(int cfg, int kg, const HaloArgs& a, hipStream_t s) {               \
+    if (kg == 2) {                                                                          \
+      switch (cfg) {                                                                        \
+        case 3: launch_tile<KS, 128, 4, 2, true, D3, 2>(a, s); break;                       \
+        case 4: launch_tile<KS, 128, 2, 2, true, D3, 2>(a, s); break;                       \
+        case 5: launch_tile<KS, 64, 4, 1, true, D3, 2>(a, s); break;                        \
+        case 7: launch_tile<KS, 32, 4, 1, true, D3, 2>(a, s); break;                        \
+        default: set_error("fsmi_conv_halo: tile %d has no K-group variant", cfg); return FSMI_ERR_ARG; \
+      }                                                                                     \
+      return finish_launch("fsmi_conv_halo");                                               \
+    }                                                                                       \
     switch (cfg) {                                                                          \
       case 0: launch_tile<KS, 64, 8, 1, false, D3>(a, s); break;                            \
       case 1: launch_tile<KS, 128, 4, 2, false, D3>(a, s); break;                           \

@@ -128,7 +128,13 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     else if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
     else cfg = Cout > 64 ? 4 : 5;
   }
-  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 9, "%s: cfg %d (0..9)", what, cfg);
+  int kg = 1;
+  if (cfg >= 16) {
+    kg = 2;
+    cfg -= 16;
+    FSMI_CHECK_ARG(halo::kg2_tile(cfg), "%s: tile %d has no K-group variant (16 + 3/4/5/7)", what, cfg);
+  }
+  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 9, "%s: cfg %d (0..9, 16 + 3/4/5/7)", what, cfg);
   switch (cfg) {                                  // tile = couts x (rows x 32 px)
     case 0: case 2: tile_counts<3, 64, 8, 1>(a); break;
     case 1: case 3: tile_counts<3, 128, 4, 2>(a); break;
@@ -152,6 +158,17 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     else if (per_split * nsplit > ws_floats) nsplit = static_cast<int>(max(1LL, ws_floats / per_split));
   }
   nsplit = max(1, min(nsplit, nck));
+  // in-block K groups (conv_halo.h, KG = 2; cfg 16 + c = tile c with K groups): the block's two
+  // wave groups split its chunks and sum through LDS -- no partials in memory, no reduce pass.
+  // FSMI_HALO_KG=2 (A/B) turns every eligible split-K >= 2 into K groups + half the splits.
+  static const int kg_env = [] {
+    const char* e = std::getenv("FSMI_HALO_KG");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (kg == 1 && kg_env == 2 && halo::kg2_tile(cfg) && nsplit >= 2) {   // A/B: fold a split of 2 into K groups
+    kg = 2;
+    nsplit = (nsplit + 1) / 2;
+  }
   a.kpc = (nck + nsplit - 1) / nsplit;
   a.nsplit = (nck + a.kpc - 1) / a.kpc;                    // no empty splits
   FSMI_CHECK_ARG(a.nsplit == 1 || (ws && per_split * a.nsplit <= ws_floats),
@@ -165,8 +182,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   }();
   a.dbg = conv_dbg;
   const bool d3 = D > 1 || KD > 1;
-  const int rc = KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, a, s) : halo::launch_cfg<3, false>(cfg, a, s))
-                         : (d3 ? halo::launch_cfg<1, true>(cfg, a, s) : halo::launch_cfg<1, false>(cfg, a, s));
+  const int rc = KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
+                         : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
   if (a.nsplit > 1) {
     const long long SP = a.cstride;

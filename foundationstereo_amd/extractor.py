@@ -147,13 +147,22 @@ class SyntheticFeature(nn.Module):
         self.args = args
         self.d_out, self.vit_dim = synth.feature_dims(args.vit_size)
         self._preset = None
+        self._by_size = {}         # (H, W) of the input images -> preset (hierarchical passes)
         self.shift_px = 0          # right-map shift of the synthesised features (no preset)
 
-    def set_features(self, left, right, vit):
-        self._preset = (list(left), list(right), vit)
+    def set_features(self, left, right, vit, size=None):
+        """Install device-resident features; with ``size=(H, W)`` only for inputs of that image
+        size (the two passes of run_hierachical see two sizes)."""
+        if size is None:
+            self._preset = (list(left), list(right), vit)
+        else:
+            self._by_size[tuple(size)] = (list(left), list(right), vit)
 
     def forward(self, x):
-        if self._preset is None:
+        hit = self._by_size.get(tuple(x.shape[-2:]))
+        if hit is not None:
+            left, right, vit = hit
+        elif self._preset is None:
             B2, _, H, W = x.shape
             fl, fr, vit = synth.backbone_features(B2 // 2, H, W, self.args.vit_size, shift_px=self.shift_px)
             left = [torch.from_numpy(a).to(x.device) for a in fl]

@@ -180,6 +180,8 @@ int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* se
  * weight fragments loaded into registers one tap ahead; 4: 128 couts x 2x32 px,
  * 5: 64 couts x 4x32 px (registers, one pixel fragment per wave: 3 waves/SIMD);
  * 8: 128 couts x 8x32 px, 9: 256 couts x 4x32 px (registers, 2x4 fragments per wave);
+ * 16 + c (c in 3, 4, 5, 7): tile c with two K groups -- 512-thread blocks whose two wave
+ * groups take alternate 32-channel chunks and sum through LDS (split-K inside the block);
  * -1: measured default.
  * nsplit: split-K over 32-channel chunks (<0: auto, sized to fill the chip);
  * partial sums go to ws (nsplit*B*Cout*H*W floats, ws_floats available) and

@@ -172,10 +172,11 @@ def test_conv2d_mfma_vs_torch(ops_mod, mode, cfg, k, cout, act):
 
 @pytest.mark.parametrize("HW", [(19, 45), (12, 40)])
 @pytest.mark.parametrize("nsplit", [1, 2])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 8, 9])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 8, 9, 19, 20, 21, 23])
 @pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (3, 136, None), (1, 129, "relu")])
 def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
-    """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2-5, 8, 9 in registers): 2 segments (16 channels + a 29-channel slice -> 2 channel
+    """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2-5, 8, 9 in registers, 16+c the
+    K-group variants: two wave groups per block on alternate chunks): 2 segments (16 channels + a 29-channel slice -> 2 channel
     chunks, ragged last chunk), ragged row/column tiles (19x45; 12x40 takes the float4 split-K
     reduce), ragged couts, output slice, every epilogue term, with and without split-K; vs fp64
     torch.  Same 2e-5 abs + 1e-5 rel tolerance as the im2col kernels."""
@@ -268,7 +269,7 @@ def test_conv3d_halo_range(ops_mod, scale, cfg):
     assert err < 3e-6, err
 
 
-@pytest.mark.parametrize("cfg", [-1, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("cfg", [-1, 5, 6, 7, 8, 9, 21, 23])
 @pytest.mark.parametrize("kern,cin,cout,D,act,res", [((3, 3, 3), 28, 28, 7, "leaky", None),
                                                      ((1, 3, 3), 28, 28, 5, "relu", None),
                                                      ((17, 1, 1), 28, 28, 20, "relu", None),

@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
-"""Measure the best tile config / split-K factor of every halo-conv shape one forward uses and
-write them to tuning/fsmi_conv.json (read by ops.conv2d / conv2d_gate / conv3d when the caller
-leaves cfg / nsplit on auto).  Run on the GPU box:
+"""Measure the best tile config / split-K factor of every halo-conv shape the given workloads use
+and MERGE them into tuning/fsmi_conv.json (read by ops.conv2d / conv2d_gate / conv3d when the
+caller leaves cfg / nsplit on auto).  Run on the GPU box:
 
-    python tools/tune_conv.py [--config cfg2] [--reps 5]
+    python tools/tune_conv.py [--config cfg2 cfg3 ...] [--reps 5] [--only-cfgs 19 20 21 23]
+
+Candidates per shape: the plain tiles (0-9 as they apply) and the K-group variants (16 + 3/4/5/7:
+two wave groups per block on alternate chunks, summed in LDS), each with split-K factors.  With
+--only-cfgs only those are timed against the shape's current table entry, the better one kept.
+Shapes of other workloads already in the table are kept as they are.
 """
 import argparse
 import json
@@ -21,7 +26,7 @@ import torch  # noqa: E402
 from foundationstereo_amd import ops, synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--config", default="cfg2")
+ap.add_argument("--config", nargs="+", default=["cfg2"])
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--only-cfgs", type=int, nargs="*", default=None,
                 help="time only these cfgs (plus the current table entry); keep the better")
@@ -29,28 +34,36 @@ ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 
-sys.path.insert(0, REPO)
 import bench  # noqa: E402  (workload table)
 
-H, W, md, iters, vit, per_gpu = bench.CONFIGS[a.config]
-args = synth.make_args(max_disp=md, corr_levels=4, vit_size=vit)
-model = bench.make_model(args, dev, 0)
-feats = [synth.backbone_features(1, H, W, vit, seed=0x5EED + i, shift_px=8) for i in range(per_gpu)]
-fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(dev) for j in range(4)]
-fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(dev) for j in range(4)]
-vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(dev)
-model.feature.set_features(fl, fr, vf)
-left, right = synth.stereo_images(per_gpu, H, W)
 
-# 1. record the shapes of one forward (tuning table disabled so every call is on auto)
-os.environ["FSMI_TUNE_DB"] = "0"
-ops._RECORD = set()
-with torch.no_grad():
-    model(torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev), iters=2, test_mode=True)
-torch.cuda.synchronize()
-keys = sorted(ops._RECORD)
-ops._RECORD = None
-print(f"[tune] {len(keys)} conv shapes", file=sys.stderr)
+def record_shapes(config):
+    """Conv shape keys of one (2-iteration) pass of ``config``, tuning table off (all on auto)."""
+    H, W, md, iters, vit, per_gpu = bench.CONFIGS[config]
+    args = synth.make_args(max_disp=md, corr_levels=4, vit_size=vit)
+    model = bench.make_model(args, dev, 0)
+    for (ph, pw) in bench.pass_sizes(config, H, W):
+        feats = [synth.backbone_features(1, ph, pw, vit, seed=0x5EED + i, shift_px=8) for i in range(per_gpu)]
+        fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(dev) for j in range(4)]
+        fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(dev) for j in range(4)]
+        vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(dev)
+        model.feature.set_features(fl, fr, vf, size=(ph, pw))
+    left, right = synth.stereo_images(per_gpu, H, W)
+    os.environ["FSMI_TUNE_DB"] = "0"
+    ops._RECORD = set()
+    with torch.no_grad():
+        lt, rt = torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev)
+        if config in bench.HIERA:
+            model.run_hierachical(lt, rt, iters=2, test_mode=True)
+        else:
+            model(lt, rt, iters=2, test_mode=True)
+    torch.cuda.synchronize()
+    keys = sorted(ops._RECORD)
+    ops._RECORD = None
+    os.environ.pop("FSMI_TUNE_DB")
+    del model
+    torch.cuda.empty_cache()
+    return keys
 
 
 def timeit(fn):
@@ -66,11 +79,14 @@ def timeit(fn):
     return e0.elapsed_time(e1) * 1e3 / a.reps
 
 
-prev = {}
-if os.path.exists(ops._TUNE_PATH):
-    with open(ops._TUNE_PATH) as f:
-        prev = json.load(f).get("entries", {})
-entries = {}
+table = {}
+if os.path.exists(a.out):
+    with open(a.out) as f:
+        table = json.load(f)
+entries = dict(table.get("entries", {}))
+prev = dict(entries)
+keys = sorted({k for c in a.config for k in record_shapes(c)})
+print(f"[tune] {len(keys)} conv shapes for {a.config}", file=sys.stderr)
 t_start = time.time()
 with torch.no_grad():
     for key in keys:
@@ -91,7 +107,8 @@ with torch.no_grad():
 
         nck = kd * ((cin + 31) // 32)
         cfgs = ([2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
-                + ([8] if cout > 64 and x.dim() == 4 else []) + ([9] if cout > 128 and x.dim() == 4 else []))
+                + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
+                + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2])
         splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck)]
         auto = timeit(lambda: run(-1, -1))
         best = (auto, -1, -1)
@@ -102,6 +119,8 @@ with torch.no_grad():
                 best = (timeit(lambda: run(old["cfg"], old["nsplit"])), old["cfg"], old["nsplit"])
         for c in cfgs:
             for s in splits:
+                if c >= 16 and 2 * s > nck:         # K groups need >= 2 chunks per block
+                    continue
                 t = timeit(lambda: run(c, s))
                 if t < best[0]:
                     best = (t, c, s)
@@ -111,7 +130,8 @@ with torch.no_grad():
                           "nsplit": best[2]}), flush=True)
 
 os.makedirs(os.path.dirname(a.out), exist_ok=True)
+configs = sorted(set(str(table.get("config", "")).split(",")) - {""} | set(a.config))
 with open(a.out, "w") as f:
-    json.dump({"device": torch.cuda.get_device_name(0), "config": a.config, "source": "tools/tune_conv.py",
-               "entries": entries}, f, indent=1, sort_keys=True)
-print(f"[tune] wrote {len(entries)} entries to {a.out} in {time.time() - t_start:.0f}s", file=sys.stderr)
+    json.dump({"device": torch.cuda.get_device_name(0), "config": ",".join(configs),
+               "source": "tools/tune_conv.py (merged per workload)", "entries": entries}, f, indent=1, sort_keys=True)
+print(f"[tune] {len(entries)} entries in {a.out} after {time.time() - t_start:.0f}s", file=sys.stderr)
