@@ -258,11 +258,13 @@ def main():
     lk_avg = lk_rep / 1e3 if lk_rep else (lk_ms / 1e3) / max(lk_n, 1)
     cb_avg = cb_rep / 1e3 if cb_rep else (cb_ms / 1e3) / max(cb_n, 1)
     traffic = traffic_build = None
-    pmc_path = os.path.join(REPO, "profiles", "pmc_lookup_summary.json")
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_lookup_summary_{a.config}.json")
+    if not os.path.exists(pmc_path):
+        pmc_path = os.path.join(REPO, "profiles", "pmc_lookup_summary.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
-        if pmc.get("config") == a.config and pmc.get("corr_levels") == L:
+        if pmc.get("config") == a.config and pmc.get("corr_levels") == L and pmc.get("pairs_per_gpu", 1) == per_gpu:
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_build = pmc.get("build_hbm_bytes_per_launch")
 

@@ -21,6 +21,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("round_dir")
 ap.add_argument("--config", default="cfg2")
 ap.add_argument("--corr-levels", type=int, default=4)
+ap.add_argument("--pairs-per-gpu", type=int, default=1)
 ap.add_argument("--out", default="profiles/pmc_lookup_summary.json")
 a = ap.parse_args()
 
@@ -44,7 +45,7 @@ for k, d in sorted(per.items()):
     print(f"{k:34s} {f:14.1f} {2 * f:12.1f} {w:14.1f} {hbm / 1e6:14.2f}")
 
 lk = [k for k in rows if k.startswith("geo_lookup_kernel")]
-summary = {"config": a.config, "corr_levels": a.corr_levels,
+summary = {"config": a.config, "corr_levels": a.corr_levels, "pairs_per_gpu": a.pairs_per_gpu,
            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), {a.round_dir}",
            "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), KB -> B x1024",
            "hbm_bytes_per_launch": rows[lk[0]]["hbm_bytes_per_launch"] if lk else None,
