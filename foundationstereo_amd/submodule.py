@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import ops, torch_ops
 
 __all__ = [
     "LayerNorm2d", "BasicConv", "Conv3dNormActReduced", "ResnetBasicBlock", "ResnetBasicBlock3D",
@@ -386,37 +386,46 @@ class Conv2x_IN(nn.Module):
 
 
 # ---------------------------------------------------------------- HIP hot path
+# The reference-API functions below dispatch through the registered operators torch.ops.fsmi.*
+# (csrc/torch_ops.cpp); the fused model internals call the C ABI through ops.py.
 
 def groupwise_correlation(fea1, fea2, num_groups):
     """core/submodule.py:388-397: the d=0 slice of the gwc volume, (B,G,H,W)."""
     B, C, H, W = fea1.shape
     assert C % num_groups == 0, f"C:{C}, num_groups:{num_groups}"
-    return ops.gwc_volume(fea1.float(), fea2.float(), 1, num_groups)[:, :, 0]
+    fea1, fea2 = fea1.float(), fea2.float()
+    return torch_ops.op("gwc_volume", fea1, fea2)(fea1, fea2, 1, num_groups)[:, :, 0]
 
 
 def build_gwc_volume(refimg_fea, targetimg_fea, maxdisp, num_groups, stride=1):
     """core/submodule.py:399-412 on the gfx950 kernel; fp32 out (the reference
     computes the correlation in fp32 and stores it in the input dtype)."""
-    out = ops.gwc_volume(refimg_fea.float(), targetimg_fea.float(), maxdisp, num_groups)
+    B, C, H, W = refimg_fea.shape
+    assert C % num_groups == 0, f"C:{C}, num_groups:{num_groups}"
+    fl, fr = refimg_fea.float(), targetimg_fea.float()
+    out = torch_ops.op("gwc_volume", fl, fr)(fl, fr, maxdisp, num_groups)
     return out if refimg_fea.dtype == torch.float32 else out.to(refimg_fea.dtype)
 
 
 def build_concat_volume(refimg_fea, targetimg_fea, maxdisp):
     """core/submodule.py:416-427 on the gfx950 kernel."""
-    out = ops.concat_volume(refimg_fea.float(), targetimg_fea.float(), maxdisp)
+    pl, pr = refimg_fea.float(), targetimg_fea.float()
+    out = torch_ops.op("concat_volume", pl, pr)(pl, pr, maxdisp)
     return out if refimg_fea.dtype == torch.float32 else out.to(refimg_fea.dtype)
 
 
 def disparity_regression(x, maxdisp):
     """core/submodule.py:431-435."""
     assert len(x.shape) == 4
-    out = ops.disparity_regression(x.float(), maxdisp)
+    xf = x.float()
+    out = torch_ops.op("disparity_regression", xf)(xf, maxdisp)
     return out if x.dtype == torch.float32 else out.to(x.dtype)
 
 
 def context_upsample(disp_low, up_weights):
     """core/submodule.py:456-468."""
-    return ops.context_upsample(disp_low.float(), up_weights.float())
+    d, w = disp_low.float(), up_weights.float()
+    return torch_ops.op("context_upsample", d, w)(d, w)
 
 
 class FeatureAtt(nn.Module):

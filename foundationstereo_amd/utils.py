@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from . import ops
+from . import torch_ops
 
 
 class InputPadder:
@@ -50,7 +50,8 @@ def bilinear_sampler(img, coords, mode="bilinear", mask=False, low_memory=False,
         assert bool((coords[..., 1] == 0).all()), "This is a stereo problem"
     P = img.shape[0]
     x = coords[..., 0].reshape(P, -1).float()
-    out = ops.bilinear_sampler_1d(img.float(), x)
+    img = img.float()
+    out = torch_ops.op("bilinear_sampler_1d", img, x)(img, x)
     out = out.reshape(P, img.shape[1], 1, -1)
     if mask:
         xg = 2 * x / (W - 1) - 1
