@@ -105,6 +105,11 @@ struct HaloArgs {
 template <int KS, bool D3>
 int launch_cfg(int cfg, int kg, const HaloArgs& a, hipStream_t s);
 
+// Pointwise tiles (cfg 24-26, conv_pw.hip): 1x1 2D layers with an LDS-DMA input ring.
+// pw_tile sets the tile geometry (a.nct = pixel tiles per image, npix, nco) before split-K.
+int launch_pw(int cfg, const HaloArgs& a, hipStream_t s);
+void pw_tile(int cfg, HaloArgs& a);
+
 // tiles with an in-block K-group (kg = 2) instantiation: the register-weight tiles that fit two
 // waves per SIMD (<= 256 VGPRs) with 512-thread blocks
 inline bool kg2_tile(int cfg) { return cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7; }

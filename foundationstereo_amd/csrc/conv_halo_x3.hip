@@ -128,14 +128,24 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     else if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
     else cfg = Cout > 64 ? 4 : 5;
   }
+  const bool d3 = D > 1 || KD > 1;
+  const bool pw = cfg >= 24;
+  if (pw) {                                        // pointwise LDS-DMA tiles (conv_pw.hip)
+    FSMI_CHECK_ARG(cfg <= 26 && KS == 1 && !d3 && HW % 4 == 0, "%s: pointwise tile %d needs a 2D 1x1 conv with "
+                   "H*W %% 4 == 0", what, cfg);
+    for (int i = 0; i < nseg; ++i)
+      FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(seg_ptr[i]) % 16 == 0, "%s: pointwise tile needs 16-B aligned "
+                     "segments", what);
+  }
   int kg = 1;
-  if (cfg >= 16) {
+  if (cfg >= 16 && !pw) {
     kg = 2;
     cfg -= 16;
     FSMI_CHECK_ARG(halo::kg2_tile(cfg), "%s: tile %d has no K-group variant (16 + 3/4/5/7)", what, cfg);
   }
-  FSMI_CHECK_ARG(cfg >= 0 && cfg <= 9, "%s: cfg %d (0..9, 16 + 3/4/5/7)", what, cfg);
-  switch (cfg) {                                  // tile = couts x (rows x 32 px)
+  FSMI_CHECK_ARG((cfg >= 0 && cfg <= 9) || pw, "%s: cfg %d (0..9, 16 + 3/4/5/7, 24..26)", what, cfg);
+  if (pw) halo::pw_tile(cfg, a);
+  else switch (cfg) {                             // tile = couts x (rows x 32 px)
     case 0: case 2: tile_counts<3, 64, 8, 1>(a); break;
     case 1: case 3: tile_counts<3, 128, 4, 2>(a); break;
     case 4: tile_counts<3, 128, 2, 2>(a); break;
@@ -181,8 +191,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     return e ? std::atoi(e) : 0;
   }();
   a.dbg = conv_dbg;
-  const bool d3 = D > 1 || KD > 1;
-  const int rc = KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
+  const int rc = pw ? halo::launch_pw(cfg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
   if (a.nsplit > 1) {

@@ -1,0 +1,273 @@
+// Pointwise (1x1) split-precision convolution with a multi-stage LDS-DMA input ring (cfg 24-26).
+//
+// A 1x1 layer gives the halo kernel one tap of MFMA work per 32-channel chunk, too little to
+// cover the chunk's global round trip with one chunk of prefetch: the loop's 1x1 layers ran at
+// 60-130 TFLOP/s against 230-300 for the 3x3 layers (tools/conv_census.py).  Here:
+//   * a block owns BM output channels x PX consecutive pixels of one image (a 1x1 conv needs no
+//     halo, so the pixel tile is a run of the flattened H*W plane: every channel row of a chunk
+//     is PX contiguous floats);
+//   * the input chunks go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging,
+//     one 1-KiB wave instruction per two 128-pixel rows) into an NS-deep ring, NS-1 chunks in
+//     flight while one is consumed; one explicit vmcnt wait + barrier per chunk;
+//   * each wave splits its own B fragments into fp16 hi / lo straight from the fp32 ring (8
+//     ds_read_b32 per fragment and k half), the weights are register-resident one chunk ahead
+//     (as conv_halo_wreg_kernel), three MFMAs per product;
+//   * range mode 2 (conv_halo.h): the block exponent is fixed from the first chunk with 8 bits of
+//     headroom; a value beyond fp16's range sets the range flag;
+//   * same split-K partials / reduce pass and the same epilogues (store_frag) as the halo tiles.
+// Entry: run_halo (conv_halo_x3.hip) with cfg 24-26; KS = 1, 2D, H*W % 4 == 0, 16-B aligned segments.
+#include "conv_halo.h"
+
+// dma16 writes m0 (the LDS-DMA base): nothing else in these kernels uses it
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace fsmi {
+namespace {
+
+// s_waitcnt with only vmcnt = N (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt 0..63");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void wait_lgkm0() {     // lgkmcnt = 0, vmcnt / expcnt untouched
+  __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (3 << 14));
+}
+
+// One LDS-DMA wave instruction: 16 B per lane from src to LDS dst + 16 * lane (dst wave-uniform).
+// Inline asm, so the compiler neither counts it nor guards the ring's LDS reads with its own
+// vmcnt(0) (it cannot tell the ring slots apart); every wait on it is explicit (wait_vmcnt).
+__device__ __forceinline__ void dma16(const float* src, float* dst) {
+  typedef __attribute__((address_space(3))) float lds_float;
+  const unsigned lds = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(reinterpret_cast<size_t>((lds_float*)dst)));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(lds) : "memory", "m0");
+}
+
+// a bare workgroup barrier: __syncthreads()' release fence would wait for vmcnt(0), i.e. for
+// every LDS-DMA chunk in flight, and serialise the ring; the waits are explicit instead
+__device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int BM, int PX, int WM, int NS>
+__global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
+  constexpr int WN = 4 / WM, TM = BM / WM / 32, TN = PX / WN / 32;
+  constexpr int CHF = HKC * PX;                    // floats per chunk: 32 channel rows x PX pixels
+  constexpr int OPS = CHF / (4 * 256);             // DMA instructions per wave per chunk (16 B a lane)
+  static_assert(TM >= 1 && TN >= 1 && OPS >= 1 && CHF % 1024 == 0 && NS >= 3, "pw tile");
+  __shared__ __attribute__((aligned(16))) float ring[NS][CHF];
+  __shared__ __attribute__((aligned(16))) float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM, hsel = lane >> 5, rl = lane & 31;
+  const long long HW = a.cstride;
+  const int nck = a.CinP / HKC;
+
+  // tile: (cout tile, split) major over an XCD-aware remap; a.nct pixel tiles per image
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int cs = item / a.npix, ptile = item - cs * a.npix;
+  const int ctile = cs / a.nsplit, split = cs - ctile * a.nsplit;
+  const int m0 = ctile * BM;
+  const int b = ptile / a.nct;
+  const long long px0 = static_cast<long long>(ptile - b * a.nct) * PX;
+  const int c_begin = split * a.kpc, c_end = min(nck, c_begin + a.kpc), n = c_end - c_begin;
+
+  // this lane's DMA elements: op o moves flat quad (wave * OPS + o) * 64 + lane of the chunk
+  int drow[OPS];
+  long long dpix[OPS];
+#pragma unroll
+  for (int o = 0; o < OPS; ++o) {
+    const int e = ((wave * OPS + o) * 64 + lane) * 4;
+    drow[o] = e / PX;
+    dpix[o] = min(px0 + e % PX, HW - 4);           // a tile tail past the plane re-reads its last quad
+  }
+  auto dma = [&](int c, int slot) FSMI_HALO_INL {
+#pragma unroll
+    for (int o = 0; o < OPS; ++o) {
+      const int ci = min(c * HKC + drow[o], a.Cin - 1);   // channels past Cin: any valid row (zeroed below)
+      const float* sp = a.seg_ptr[0];
+      long long sb = a.seg_bstride[0];
+      int base = 0;
+#pragma unroll
+      for (int q = 1; q < kHMaxSeg; ++q) {
+        const bool in_q = q < a.nseg && ci >= a.seg_end[q - 1];
+        sp = in_q ? a.seg_ptr[q] : sp;
+        sb = in_q ? a.seg_bstride[q] : sb;
+        base = in_q ? a.seg_end[q - 1] : base;
+      }
+      const float* src = sp + b * sb + static_cast<long long>(ci - base) * HW + dpix[o];
+      dma16(src, &ring[slot][(wave * OPS + o) * 256]);
+    }
+  };
+
+  int wrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) wrow[i] = min(m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
+  half8 wf[2][TM][2][2];                           // [buffer][i][k half][hi, lo]
+  auto load_wf = [&](auto buf_c, int c) FSMI_HALO_INL {
+    constexpr int buf = decltype(buf_c)::value;
+    const size_t base = static_cast<size_t>(c) * a.CoutP * HKC;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
+        wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+      }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  bool pix_ok[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) pix_ok[j] = px0 + (wn * TN + j) * 32 + rl < HW;
+
+  float scale = 1.f;
+  int sx = kNoExp;
+  bool ovf = false;
+  // prologue: weights of the first chunk, then NS - 1 chunks in flight
+  if (n > 0) {
+    load_wf(std::integral_constant<int, 0>(), c_begin);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) dma(min(c_begin + s, c_end - 1), s);
+  }
+  // chunk q (buffer parity P): prefetch weights q+1 and chunk q+NS-1, wait for chunk q and
+  // weights q (the 2*OPS + 4*TM younger memory ops may stay in flight), barrier, MFMAs, barrier
+  auto step = [&](auto par_c, int q) FSMI_HALO_INL {
+    constexpr int P = decltype(par_c)::value;
+    const int c = c_begin + q;
+    load_wf(std::integral_constant<int, P ^ 1>(), min(c + 1, c_end - 1));
+    dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
+    wait_vmcnt<2 * OPS + 4 * TM>();                // this wave's part of chunk q has landed
+    bar();                                         // ... and every wave's
+    const float* xs = ring[q % NS];
+    if (q == 0) {                                  // block exponent from the first chunk (range mode 2)
+      float m = 0.f;
+#pragma unroll
+      for (int u = 0; u < CHF / 1024; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(xs + (u * 256 + tid) * 4);
+        const int row = ((u * 256 + tid) * 4) / PX;
+        const bool okc = c * HKC + row < a.Cin;
+        m = fmaxf(m, okc ? fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) : 0.f);
+      }
+      m = wave_max(m);
+      if (lane == 0) red[wave] = m;
+      wait_lgkm0();
+      bar();
+      sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
+      scale = exp2i(sx == kNoExp ? 0 : sx);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        ah[i] = wf[P][i][k][0];
+        al[i] = wf[P][i][k][1];
+      }
+      const int ci0 = 16 * k + 8 * hsel;
+      const int nvalid = a.Cin - c * HKC - ci0;    // channels of this lane's 8 that exist
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int pl = (wn * TN + j) * 32 + rl;
+        f32x8 x;
+        float mx = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float v = xs[(ci0 + t) * PX + pl];
+          x[t] = (t < nvalid && pix_ok[j]) ? v * scale : 0.f;
+          mx = fmaxf(mx, fabsf(x[t]));
+        }
+        ovf |= mx >= 65504.f;
+        bh[j] = __builtin_convertvector(x, half8);
+        bl[j] = __builtin_convertvector(x - __builtin_convertvector(bh[j], f32x8), half8);
+      }
+      mma3<TM, TN>(acc, ah, al, bh, bl);
+    }
+    wait_lgkm0();
+    bar();                                         // every wave is done with slot q % NS
+  };
+  int q = 0;
+  for (; q + 1 < n; q += 2) {
+    step(std::integral_constant<int, 0>(), q);
+    step(std::integral_constant<int, 1>(), q + 1);
+  }
+  if (q < n) step(std::integral_constant<int, 0>(), q);
+  wait_vmcnt<0>();                                 // the tail's clamped prefetches land before exit
+  flag_overflow(a, ovf);
+
+  const float xinv = exp2i(sx == kNoExp ? 0 : -sx);
+  if (a.nsplit > 1) {                              // raw partials (packed units) into ws slot `split`
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (!pix_ok[j]) continue;
+      const long long hw = px0 + (wn * TN + j) * 32 + rl;
+      float* wp = a.ws + (static_cast<size_t>(split) * a.B + b) * a.Cout * HW + hw;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+          if (co < a.Cout) wp[static_cast<size_t>(co) * HW] = acc[i][j][r] * xinv;
+        }
+    }
+    return;
+  }
+  auto epi = [&](auto act_c) FSMI_HALO_INL {
+    constexpr int ACT = decltype(act_c)::value;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (!pix_ok[j]) continue;
+      const long long hw = px0 + (wn * TN + j) * 32 + rl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        store_frag<ACT, false>(a, acc[i][j], xinv, m0 + (wm * TM + i) * 32 + 4 * hsel, b, hw, a.out, a.sb, a.gamma,
+                               a.res, a.gh, a.gz, a.gatt, a.grh);
+    }
+  };
+  switch (a.act) {
+    case 1: epi(std::integral_constant<int, 1>()); break;
+    case 2: epi(std::integral_constant<int, 2>()); break;
+    case 3: epi(std::integral_constant<int, 3>()); break;
+    case 4: epi(std::integral_constant<int, 4>()); break;
+    case 5: epi(std::integral_constant<int, 5>()); break;
+    case 6: epi(std::integral_constant<int, 6>()); break;
+    default: epi(std::integral_constant<int, 0>()); break;
+  }
+}
+
+}  // namespace
+
+namespace halo {
+
+// cfg 24: 128 couts x 128 px (2 x 2 fragments per wave), 3-deep ring; 25: 128 x 64 (2 x 1), 4 deep;
+// 26: 64 x 128 (2 x 1, waves along the pixels), 3 deep.  Deeper rings (6 / 8 chunks, 64-96 KB of
+// LDS) measured 5-40 % slower on every cfg2 1x1 shape (tools/pw_bench.py), so the chunk round
+// trip is not what bounds these layers.  Tile geometry (a.nct = pixel tiles per image, a.npix, a.nco) is set by
+// the caller (pw_tile).
+int launch_pw(int cfg, const HaloArgs& a, hipStream_t s) {
+  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
+  switch (cfg) {
+    case 24: hipLaunchKernelGGL((conv_pw_kernel<128, 128, 2, 3>), dim3(grid), dim3(256), 0, s, a); break;
+    case 25: hipLaunchKernelGGL((conv_pw_kernel<128, 64, 2, 4>), dim3(grid), dim3(256), 0, s, a); break;
+    case 26: hipLaunchKernelGGL((conv_pw_kernel<64, 128, 1, 3>), dim3(grid), dim3(256), 0, s, a); break;
+    default: set_error("fsmi_conv_halo: pointwise tile %d (24..26)", cfg); return FSMI_ERR_ARG;
+  }
+  return finish_launch("fsmi_conv_halo");
+}
+
+void pw_tile(int cfg, HaloArgs& a) {
+  const int BM = cfg == 26 ? 64 : 128, PX = cfg == 25 ? 64 : 128;
+  const long long HW = a.cstride;
+  a.nrt = 1;
+  a.nct = static_cast<int>((HW + PX - 1) / PX);
+  a.npix = a.B * a.nct;
+  a.nco = (a.Cout + BM - 1) / BM;
+}
+
+}  // namespace halo
+}  // namespace fsmi

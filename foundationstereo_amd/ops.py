@@ -455,8 +455,11 @@ def _tune_key(ks, kd, cin, cout, B, D, H, W) -> str:
 def _tuned(ks, kd, cin, cout, B, D, H, W, cfg, nsplit):
     global _TUNE
     key = _tune_key(ks, kd, cin, cout, B, D, H, W)
-    if _RECORD is not None:
-        _RECORD.add(key)
+    if _RECORD is not None:           # a set (shape keys) or a dict (call counts, tools/conv_census.py)
+        if isinstance(_RECORD, dict):
+            _RECORD[key] = _RECORD.get(key, 0) + 1
+        else:
+            _RECORD.add(key)
     if cfg >= 0 and nsplit >= 0 or os.environ.get("FSMI_TUNE_DB", "1") == "0":
         return cfg, nsplit
     if _TUNE is None:

@@ -64,6 +64,7 @@ def synth_features(vit, shift):
     return features
 
 
+@pytest.mark.timeout(900)             # the CPU oracle at full size takes minutes
 @pytest.mark.parametrize("name,H,W,md,iters,vit,B", [
     ("cfg3_per_gpu", 480, 640, 192, 32, "vitl", 4),
     ("cfg4", 384, 1248, 256, 32, "vitl", 1),
@@ -86,6 +87,7 @@ def test_config_vs_oracle(lib, name, H, W, md, iters, vit, B):
     assert max(per_pair) < 1e-3, f"max |dd| per pair vs oracle = {per_pair} px"
 
 
+@pytest.mark.timeout(900)             # the CPU oracle at full size takes minutes
 def test_hierarchical_vs_reference_golden(lib):
     """run_hierachical at 200x300 (coarse 100x150 -> 128x160, fine 224x320, _pad[0] = 10) vs the
     reference's own run_hierachical (tests/golden/hiera_small.npz)."""
@@ -103,6 +105,7 @@ def test_hierarchical_vs_reference_golden(lib):
     assert d < 1e-3, f"max |dd| vs reference = {d} px"
 
 
+@pytest.mark.timeout(900)             # the CPU oracle at full size takes minutes
 def test_cfg5_hierarchical_vs_oracle(lib):
     """cfg5 at full size: 1536x1024 --hiera, D320 (D4 = 80: 20 transformer tokens), ViT-L, 22
     iterations, both passes, vs the oracle's run_hierachical restatement."""
@@ -123,6 +126,7 @@ def test_cfg5_hierarchical_vs_oracle(lib):
     assert d < 1e-3, f"max |dd| vs oracle = {d} px"
 
 
+@pytest.mark.timeout(900)             # the CPU oracle at full size takes minutes
 def test_autocast_keeps_hip_convs(lib):
     """The reference runs its forward under fp16 autocast (scripts/run_demo.py:161).  Under
     autocast the same halo-kernel convs must run (identical algorithmic conv FLOPs counted by
@@ -189,6 +193,7 @@ def _rescale_activations_(m, c_big=1e4, c_small=1e-4):
     return m
 
 
+@pytest.mark.timeout(900)             # the CPU oracle at full size takes minutes
 def test_e2e_activation_range_vs_oracle(lib):
     """cfg1 geometry (320x256, D64, 8 iterations, L=4) with the activations between homogeneous
     layer pairs moved to ~1e4 and ~1e-4 (function-preserving, _rescale_activations_): the HIP path

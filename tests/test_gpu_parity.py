@@ -199,6 +199,55 @@ def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
 
 
+@pytest.mark.parametrize("HW", [(12, 40), (16, 64)])
+@pytest.mark.parametrize("nsplit", [1, 2, 3])
+@pytest.mark.parametrize("cfg", [24, 25, 26])
+@pytest.mark.parametrize("cout,act,wide", [(70, "gelu", False), (129, "relu", True), (256, None, True)])
+def test_conv2d_pw_vs_torch(ops_mod, cfg, cout, act, wide, nsplit, HW):
+    """Pointwise LDS-DMA tiles (conv_pw.hip, cfg 24-26): 2 or 3 segments (16 channels, optionally
+    160 more, a 29-channel slice: 2 or 7 chunks through the 3/4-deep ring, ragged last chunk), pixel
+    tiles past the plane end (480 px), ragged couts, output slice, every epilogue term, split-K;
+    vs fp64 torch, same tolerance as the halo tiles."""
+    import torch.nn.functional as F
+    B, (H, W) = 2, HW
+    a_ = synth.normal(291, (B, 16, H, W))
+    c_ = synth.normal(292, (B, 40, H, W))
+    e_ = synth.normal(297, (B, 160, H, W)) if wide else None
+    cin = 45 + (160 if wide else 0)
+    w = synth.normal(293, (cout, cin, 1, 1), 0.2)
+    bias = synth.normal(294, (cout,), 0.1)
+    gamma = synth.uniform(295, (cout,), 0.5, 1.5)
+    res = synth.normal(296, (B, cout, H, W))
+    segs = [g(a_)] + ([g(e_)] if wide else []) + [(g(c_), 5, 29)]      # inner segments: multiples of 8
+    x = torch.cat([t(a_)] + ([t(e_)] if wide else []) + [t(c_[:, 5:34])], 1)
+    out = torch.zeros(B, cout + 3, H, W, device=DEV)
+    ops_mod.conv2d(segs, ops_mod.PackedConv(g(w), mode="halo"), bias=g(bias), act=act, alpha=0.75,
+                   gamma=g(gamma), res=g(res), out=out, co0=2, cfg=cfg, nsplit=nsplit)
+    y = F.conv2d(x.double(), t(w).double(), t(bias).double())
+    y = {"relu": F.relu, "gelu": F.gelu, None: lambda v: v}[act](y)
+    ref = t(res).double() + t(gamma).double().view(1, -1, 1, 1) * 0.75 * y
+    close(out[:, 2:2 + cout], ref, atol=2e-5, rtol=1e-5)
+    assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
+
+
+@pytest.mark.parametrize("scale", [3e5, 1e3, 1e-4, 1e-7])
+@pytest.mark.parametrize("cfg", [24, 25, 26])
+def test_conv2d_pw_range(ops_mod, scale, cfg):
+    """Pointwise tiles keep ~22 bits across input scales (block exponent from the first chunk)."""
+    import torch.nn.functional as F
+    B, H, W, cin, cout = 1, 16, 40, 96, 130
+    x = synth.normal(391, (B, cin, H, W)) * scale
+    w = synth.normal(392, (cout, cin, 1, 1), 0.2)
+    ops_mod.range_overflowed(reset=True)
+    ref = F.conv2d(t(x).double(), t(w).double())
+    for nsplit in (1, 2):
+        out = ops_mod.conv2d([g(x)], ops_mod.PackedConv(g(w), mode="halo"), cfg=cfg, nsplit=nsplit)
+        assert bool(torch.isfinite(out).all())
+        err = float((out.double().cpu() - ref).abs().max() / ref.abs().max())
+        assert err < 3e-6, (nsplit, err)
+    assert not ops_mod.range_overflowed(reset=True)
+
+
 @pytest.mark.parametrize("scale", [3e5, 1e3, 1e-4, 1e-7])
 @pytest.mark.parametrize("cfg", [-1, 1, 3, 4, 9])
 @pytest.mark.parametrize("k", [1, 3])

@@ -115,5 +115,7 @@ def test_conv_tuning_db_wellformed():
         ks, kd, cin, cout, B, D, H, W = (int(v) for v in re.findall(r"\d+", key))
         assert key == ops._tune_key(ks, kd, cin, cout, B, D, H, W)
         assert ks in (1, 3) and kd % 2 == 1 and min(cin, cout, B, D, H, W) > 0
-        # plain tiles 0..9 (all legal on volumes too) or the K-group variants 16 + 3/4/5/7
-        assert (0 <= e["cfg"] <= 9 or e["cfg"] in (19, 20, 21, 23)) and 1 <= e["nsplit"] <= 8, (key, e)
+        # plain tiles 0..9 (all legal on volumes too), the K-group variants 16 + 3/4/5/7, or the
+        # pointwise tiles 24..26 (2D 1x1 layers only)
+        assert (0 <= e["cfg"] <= 9 or e["cfg"] in (19, 20, 21, 23)
+                or (24 <= e["cfg"] <= 26 and ks == 1 and kd == 1 and D == 1)) and 1 <= e["nsplit"] <= 8, (key, e)

@@ -27,6 +27,8 @@ dev = torch.device("cuda:0")
 # (name, cin, cout, (kd, k, k), D, H, W)
 SHAPES = [
     ("stem.3x3x3", 28, 28, (3, 3, 3), 48, 120, 160),
+    ("cls.3x3x3.28-14", 28, 14, (3, 3, 3), 48, 120, 160),
+    ("cls.3x3x3.14-14", 14, 14, (3, 3, 3), 48, 120, 160),
     ("apc.1x3x3", 28, 28, (1, 3, 3), 48, 120, 160),
     ("apc.17x1x1", 28, 28, (17, 1, 1), 48, 120, 160),
     ("hg1.1x3x3", 56, 56, (1, 3, 3), 24, 60, 80),
@@ -61,7 +63,10 @@ with torch.no_grad():
         if not a.no_miopen:
             row["miopen_us"] = round(timeit(lambda: F.relu(F.conv3d(x, w, b, padding=tuple(q // 2 for q in k)))), 1)
         row["auto_us"] = round(timeit(lambda: ops.conv3d(x, pk, bias=b, act="relu")), 1)
+        ref = F.relu(F.conv3d(x, w, b, padding=tuple(q // 2 for q in k)))
         for c in a.cfgs:
             row[f"cfg{c}_us"] = round(timeit(lambda: ops.conv3d(x, pk, bias=b, act="relu", cfg=c)), 1)
+            y = ops.conv3d(x, pk, bias=b, act="relu", cfg=c)
+            row[f"cfg{c}_err"] = float(((y - ref).abs().max() / ref.abs().max()).item())
         row["auto_TF"] = round(fl / row["auto_us"] / 1e6, 1)
         print(json.dumps(row), flush=True)

@@ -5,8 +5,9 @@ caller leaves cfg / nsplit on auto).  Run on the GPU box:
 
     python tools/tune_conv.py [--config cfg2 cfg3 ...] [--reps 5] [--only-cfgs 19 20 21 23]
 
-Candidates per shape: the plain tiles (0-9 as they apply) and the K-group variants (16 + 3/4/5/7:
-two wave groups per block on alternate chunks, summed in LDS), each with split-K factors.  With
+Candidates per shape: the plain tiles (0-9 as they apply), the K-group variants (16 + 3/4/5/7:
+two wave groups per block on alternate chunks, summed in LDS) and for 2D 1x1 layers the pointwise
+LDS-DMA tiles (24-26, conv_pw.hip), each with split-K factors.  With
 --only-cfgs only those are timed against the shape's current table entry, the better one kept.
 Shapes of other workloads already in the table are kept as they are.
 """
@@ -30,6 +31,7 @@ ap.add_argument("--config", nargs="+", default=["cfg2"])
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--only-cfgs", type=int, nargs="*", default=None,
                 help="time only these cfgs (plus the current table entry); keep the better")
+ap.add_argument("--match", default="", help="only re-tune shape keys matching this regex (e.g. '_d(?!1_)' volumes)")
 ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
 a = ap.parse_args()
 dev = torch.device("cuda:0")
@@ -67,16 +69,25 @@ def record_shapes(config):
 
 
 def timeit(fn):
+    """GPU time per call: reps calls captured into one hipGraph and replayed (as bench.py runs the
+    forward), so small layers are not timed at the host's launch rate (~17 us per eager call)."""
     fn()
     fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(a.reps):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(a.reps):
-        fn()
+    for _ in range(3):
+        g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1e3 / a.reps
+    del g
+    return e0.elapsed_time(e1) * 1e3 / (3 * a.reps)
 
 
 table = {}
@@ -86,6 +97,8 @@ if os.path.exists(a.out):
 entries = dict(table.get("entries", {}))
 prev = dict(entries)
 keys = sorted({k for c in a.config for k in record_shapes(c)})
+if a.match:
+    keys = [k for k in keys if re.search(a.match, k)]
 print(f"[tune] {len(keys)} conv shapes for {a.config}", file=sys.stderr)
 t_start = time.time()
 with torch.no_grad():
@@ -108,7 +121,8 @@ with torch.no_grad():
         nck = kd * ((cin + 31) // 32)
         cfgs = ([2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
-                + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2])
+                + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
+                + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
         splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck)]
         auto = timeit(lambda: run(-1, -1))
         best = (auto, -1, -1)
