@@ -472,12 +472,19 @@ def _tuned(ks, kd, cin, cout, B, D, H, W, cfg, nsplit):
         cfg, nsplit = (e["cfg"] if cfg < 0 else cfg), (e["nsplit"] if nsplit < 0 else nsplit)
     if _SPLIT_MAXPIX and kd == 1 and D == 1 and H * W <= _SPLIT_MAXPIX:
         nsplit = 1
+    if _SPLIT_CAP and nsplit > _SPLIT_CAP:
+        nsplit = _SPLIT_CAP
     return cfg, nsplit
 
 
 # A/B knob: no split-K for 2D maps of at most this many pixels (the 1/8 and 1/16 GRU levels run on
 # a side stream beside gru04, so the chip is already busy and split-K only adds the reduce pass)
 _SPLIT_MAXPIX = int(os.environ.get("FSMI_SPLIT_MAXPIX", "0"))
+# Cap on the split-K factor of auto-chosen layers (0: none).  The table is timed one layer at a
+# time on an idle chip; inside the 4-stream pipelined loop other streams' kernels fill the CUs that
+# a deep split was chosen to fill, and the extra partial-sum traffic remains.  Measured end to end
+# (cfg2, two runs each): cap 2 +1.3 %, cap 3 -1.2 %, cap 1 -12 %; cfg3 (4 pairs / GPU) neutral.
+_SPLIT_CAP = int(os.environ.get("FSMI_SPLIT_CAP", "2"))
 
 
 _SPLIT_WS = {}

@@ -31,6 +31,7 @@ ap.add_argument("--config", nargs="+", default=["cfg2"])
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--only-cfgs", type=int, nargs="*", default=None,
                 help="time only these cfgs (plus the current table entry); keep the better")
+ap.add_argument("--max-split", type=int, default=8, help="largest split-K factor to time")
 ap.add_argument("--match", default="", help="only re-tune shape keys matching this regex (e.g. '_d(?!1_)' volumes)")
 ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
 a = ap.parse_args()
@@ -123,7 +124,7 @@ with torch.no_grad():
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
                 + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
                 + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
-        splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck)]
+        splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck) and s <= a.max_split]
         auto = timeit(lambda: run(-1, -1))
         best = (auto, -1, -1)
         if a.only_cfgs is not None:
