@@ -28,6 +28,8 @@ SIGNATURES = {
     "fsmi_allpairs_corr": [_P, _P, _PP, _I, _I, _I, _I, _I, _P, _P],
     "fsmi_volume_pyramid": [_P, _PP, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_geo_lookup": [_PP, _PP, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_conv1x1_lookup": [_PP, _PP, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P,
+                            ctypes.c_longlong, _P],
     "fsmi_bilinear_sampler_1d": [_P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_disparity_regression": [_P, _P, _I, _I, _I, _I, _P],
     "fsmi_softmax_regression": [_P, _P, _I, _I, _I, _I, _P],

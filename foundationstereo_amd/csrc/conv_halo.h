@@ -108,6 +108,8 @@ int launch_cfg(int cfg, int kg, const HaloArgs& a, hipStream_t s);
 // Pointwise tiles (cfg 24-26, conv_pw.hip): 1x1 2D layers with an LDS-DMA input ring.
 // pw_tile sets the tile geometry (a.nct = pixel tiles per image, npix, nco) before split-K.
 int launch_pw(int cfg, const HaloArgs& a, hipStream_t s);
+// split-K reduce pass over a.ws (conv_halo_x3.hip)
+void split_reduce(const HaloArgs& a, hipStream_t s);
 void pw_tile(int cfg, HaloArgs& a);
 
 // tiles with an in-block K-group (kg = 2) instantiation: the register-weight tiles that fit two

@@ -67,6 +67,27 @@ void tile_counts(HaloArgs& a) {
 }  // namespace
 }  // namespace fsmi
 
+namespace fsmi {
+namespace halo {
+
+// the split-K reduce pass of a launch whose partials are in a.ws (also used by conv_lookup.hip)
+void split_reduce(const HaloArgs& a, hipStream_t s) {
+  const long long SP = a.cstride;
+  const bool vec = SP % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(a.ws) % 16 == 0 &&
+                   (!a.res || reinterpret_cast<uintptr_t>(a.res) % 16 == 0);
+  if (vec) {
+    hipLaunchKernelGGL(conv_split_reduce4_kernel, dim3(static_cast<unsigned>((SP / 4 + 255) / 256), a.B * a.Cout),
+                       dim3(256), 0, s, a);
+  } else {
+    const long long n = static_cast<long long>(a.B) * a.Cout * SP;
+    hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, a);
+  }
+}
+
+}  // namespace halo
+}  // namespace fsmi
+
 using namespace fsmi;
 
 
@@ -194,20 +215,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   const int rc = pw ? halo::launch_pw(cfg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
-  if (a.nsplit > 1) {
-    const long long SP = a.cstride;
-    const bool vec = SP % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
-                     reinterpret_cast<uintptr_t>(a.ws) % 16 == 0 &&
-                     (!a.res || reinterpret_cast<uintptr_t>(a.res) % 16 == 0);
-    if (vec) {
-      hipLaunchKernelGGL(conv_split_reduce4_kernel, dim3(static_cast<unsigned>((SP / 4 + 255) / 256), a.B * a.Cout),
-                         dim3(256), 0, s, a);
-    } else {
-      const long long n = static_cast<long long>(a.B) * a.Cout * SP;
-      hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
-                         a);
-    }
-  }
+  if (a.nsplit > 1) halo::split_reduce(a, s);
   return finish_launch(what);
 }
 

@@ -3,6 +3,7 @@
 // in the epilogue, the D pyramid of the filtered volume read in its native
 // NCDHW layout (no permute copy), and the fused multi-level 9-tap lookup.
 #include "fsmi_common.h"
+#include "lookup_taps.h"
 
 namespace fsmi {
 namespace {
@@ -257,64 +258,6 @@ struct LookupArgs {
   float* out;
   int L, Cv, D, H, W, W2, B;
   unsigned long long* clk;   // in-kernel launch clock (nullptr: off)
-};
-
-// FP contraction is OFF for the coordinate math: fusing `ix - floor(ix)` into
-// fma(h, x'+1, -floor) computes the fraction from the UNROUNDED ix and moves
-// samples near integer positions by up to an ulp of ix (seen as 1e-5 errors
-// at x ~ 80 on gfx950 before this pragma).
-__device__ __forceinline__ float unnorm(float x, int n) {
-#pragma clang fp contract(off)
-  const float xn = (2.f * x) / static_cast<float>(n - 1) - 1.f;
-  return (xn + 1.f) * (static_cast<float>(n - 1) / 2.f);
-}
-
-// The 2r+1 taps of one (pixel, level): window base, per-tap fraction and which
-// window pair each tap reads.  Channel-independent, so computed once and
-// reused for every channel of the level (the division lives here).
-template <int R>
-struct Taps {
-  static constexpr int K = 2 * R + 1, NW = 2 * R + 4;
-  int xb;            // window covers [xb, xb + NW)
-  float f[K];        // fraction of tap k
-  int sel[K];        // tap k interpolates win[k+sel], win[k+sel+1], sel in {0,1,2}
-  bool lo, hi;       // window ends needed (only when a tap's round trip crossed an integer)
-
-  __device__ __forceinline__ void init(float xc, int n) {
-#pragma clang fp contract(off)
-    // xc = centre coordinate (tap k sits at xc + (k - R)); clamp keeps int math defined
-    const float xcl = fminf(fmaxf(xc, -1.0e6f), 1.0e6f);
-    xb = static_cast<int>(floorf(xcl)) - R - 1;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float ix = unnorm(static_cast<float>(k - R) + xcl, n);
-      const float fl = floorf(ix);
-      f[k] = ix - fl;
-      sel[k] = static_cast<int>(fl) - xb - k;
-    }
-    lo = sel[0] == 0;       // only tap 0 can reach win[0]
-    hi = sel[K - 1] == 2;   // only tap 2r can reach win[2r+3]
-  }
-
-  __device__ __forceinline__ void sample(const float* __restrict__ src, size_t stride, int n,
-                                         float* __restrict__ dst, size_t dstride) const {
-#pragma clang fp contract(off)
-    // the 2r+2 window elements every tap set touches, plus the two ends only for lanes whose
-    // taps need them: HBM sees the algorithmic 2r+2 loads per channel
-    float win[NW];
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const int x = xb + j;
-      const bool need = (j == 0) ? lo : ((j == NW - 1) ? hi : true);
-      win[j] = (need && x >= 0 && x < n) ? src[static_cast<size_t>(x) * stride] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const float v0 = sel[k] == 0 ? win[k] : (sel[k] == 1 ? win[k + 1] : win[k + 2]);
-      const float v1 = sel[k] == 0 ? win[k + 1] : (sel[k] == 1 ? win[k + 2] : win[k + 3]);
-      dst[static_cast<size_t>(k) * dstride] = v0 * (1.f - f[k]) + v1 * f[k];
-    }
-  }
 };
 
 template <int R>

@@ -440,6 +440,66 @@ def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Te
     del keep
 
 
+def lookup_channel_order(L: int, Cv: int, radius: int = 4) -> Tensor:
+    """Input-channel order of ``fsmi_conv1x1_lookup``: the index, in the lookup's channel layout
+    (core/geometry.py:62-65: per level [geo c*K + k ..., corr k ...], K = 2r+1), of each kernel
+    channel (-1: a zero row).  Chunk q of 32 holds groups 3q..3q+2 (group = level*(Cv+1) + c)."""
+    K = 2 * radius + 1
+    gpc = 32 // K
+    G = L * (Cv + 1)
+    nck = (G + gpc - 1) // gpc
+    order = torch.full((nck * 32,), -1, dtype=torch.long)
+    for g in range(G):
+        i, c = divmod(g, Cv + 1)
+        for k in range(K):
+            order[(g // gpc) * 32 + (g % gpc) * K + k] = i * K * (Cv + 1) + c * K + k
+    return order
+
+
+def pack_lookup_conv(weight: Tensor, L: int, Cv: int, radius: int = 4) -> "PackedConv":
+    """convc1's (Cout, L*K*(Cv+1), 1, 1) weight re-ordered for ``fsmi_conv1x1_lookup`` and packed."""
+    order = lookup_channel_order(L, Cv, radius).to(weight.device)
+    w = weight.detach().float().reshape(weight.shape[0], -1)
+    assert w.shape[1] == L * (2 * radius + 1) * (Cv + 1), "pack_lookup_conv: channel count"
+    wn = torch.zeros(w.shape[0], order.numel(), device=w.device, dtype=w.dtype)
+    m = order >= 0
+    wn[:, m] = w[:, order[m]]
+    return PackedConv(wn.reshape(w.shape[0], -1, 1, 1), mode="halo")
+
+
+def conv1x1_lookup(vol_levels: Sequence[Tensor], corr_levels: Sequence[Tensor], disp: Tensor, radius: int,
+                   pk: "PackedConv", bias: Tensor = None, act=None, out: Tensor = None, co0: int = 0,
+                   nsplit: int = 2) -> Tensor:
+    """act(conv1x1(geo_lookup(vol_levels, corr_levels, disp, radius)) + bias) without the lookup
+    tensor (``fsmi_conv1x1_lookup``); ``pk`` from ``pack_lookup_conv``."""
+    _check("conv1x1_lookup", disp, *vol_levels, *corr_levels)
+    L = len(vol_levels)
+    B, Cv, D, H, W = vol_levels[0].shape
+    W2 = corr_levels[0].shape[-1]
+    assert disp.shape == (B, 1, H, W), f"disp {tuple(disp.shape)} vs volume {(B, 1, H, W)}"
+    for i in range(L):
+        assert vol_levels[i].shape == (B, Cv, D >> i, H, W) and vol_levels[i].is_contiguous()
+        assert corr_levels[i].shape == (B, H, W, W2 >> i) and corr_levels[i].is_contiguous()
+    K = 2 * radius + 1
+    assert pk.mode == "halo" and pk.k == 1 and pk.cin == lookup_channel_order(L, Cv, radius).numel(), \
+        "conv1x1_lookup: weights must come from pack_lookup_conv"
+    disp = _c(disp)
+    if out is None:
+        out = torch.empty((B, pk.cout, H, W), device=disp.device, dtype=torch.float32)
+    assert out.is_contiguous() and out.shape[0] == B and out.shape[2:] == (H, W)
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * L * K * (Cv + 1) * pk.cout * B * H * W
+    stream = _stream(disp)
+    ws = _split_workspace(disp.device, stream, 8 * B * pk.cout * H * W)
+    pv, kv = _lib.ptr_array([_p(t) for t in vol_levels])
+    pc, kc = _lib.ptr_array([_p(t) for t in corr_levels])
+    _lib.check(_lib.load().fsmi_conv1x1_lookup(
+        pv, pc, _p(disp), L, radius, B, Cv, D, H, W, W2, _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
+        _p(out), out.shape[1], co0, pk.cout, ACT[act], nsplit, _p(ws), ws.numel(), stream), "conv1x1_lookup")
+    del kv, kc
+    return out
+
+
 # ---- measured tile / split-K choices per conv shape (tools/tune_conv.py -> tuning/fsmi_conv.json):
 # consulted when a caller leaves cfg / nsplit on auto; shapes not in the table use the C-side policy
 _TUNE_PATH = os.environ.get("FSMI_TUNE_PATH") or os.path.join(

@@ -95,6 +95,20 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
                     int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
                     void* stream);
 
+/* ---- a6 + a7: lookup fused into the motion encoder's convc1 ------------------
+ * replaces core/update.py:62 F.relu(self.convc1(corr)) with corr = the lookup above
+ * (core/geometry.py:43-65): out[b, co0+co] = act(bias[co] + sum_ch W[co, ch] lookup[b, ch])
+ * without materialising the lookup.  Arguments of fsmi_geo_lookup (radius 4), then a
+ * 1x1 conv in fsmi_conv2d_halo_x3's packing whose input channels follow the chunk
+ * order of the kernel: chunk q = groups 3q..3q+2 (group g = level*(Cv+1) + c, c == Cv the
+ * correlation group) as channels (g-3q)*9 + k, channels 27..31 zero
+ * (ops.pack_lookup_conv).  Cout <= 256; act 0 none / 1 ReLU; nsplit split-K factor
+ * (partials in ws, B*Cout*H*W floats each). */
+int fsmi_conv1x1_lookup(const float* const* vol_levels, const float* const* corr_levels, const float* disp,
+                        int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
+                        const void* whi, const void* wlo, const float* scale_bias, float* out, int out_ctot,
+                        int co0, int Cout, int act, int nsplit, float* ws, long long ws_floats, void* stream);
+
 /* 1-D stereo specialisation of bilinear_sampler (core/utils/utils.py:44-55):
  * img (P,C,1,Lx); x (P,K) pixel x-coordinates (y == 0); out (P,C,1,K). */
 int fsmi_bilinear_sampler_1d(const float* img, const float* x, float* out,

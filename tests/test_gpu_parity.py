@@ -230,6 +230,32 @@ def test_conv2d_pw_vs_torch(ops_mod, cfg, cout, act, wide, nsplit, HW):
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
 
 
+@pytest.mark.parametrize("L,Cv,D,H,W,B,nsplit", [(4, 28, 48, 12, 40, 1, 1), (2, 8, 24, 5, 37, 2, 2),
+                                                   (4, 28, 48, 30, 40, 1, 3), (3, 28, 80, 7, 64, 1, 2)])
+def test_conv1x1_lookup_vs_unfused(ops_mod, L, Cv, D, H, W, B, nsplit):
+    """convc1 with the lookup fused into its staging (fsmi_conv1x1_lookup) vs geo_lookup + the halo
+    1x1 conv on the same inputs and weights: disparities below 0, beyond D and on integers, ragged
+    pixel tiles (H*W not a multiple of 64), batch 2, split-K; within the split-precision tolerance."""
+    import torch.nn.functional as F
+    r, K = 4, 9
+    gen = torch.Generator().manual_seed(31 + L + Cv)
+    vol = torch.randn(B, Cv, D, H, W, generator=gen).to(DEV)
+    fl, fr = (torch.randn(B, 32, H, W, generator=gen).to(DEV) for _ in range(2))
+    corr = ops_mod.allpairs_corr(fl, fr, L)
+    pyr = ops_mod.volume_pyramid(vol, L)
+    disp = (torch.rand(B, 1, H, W, generator=gen) * (D + 8) - 4).to(DEV)
+    disp[..., 0, :3] = torch.tensor([0.0, 5.0, float(D - 1)], device=DEV)
+    cin = L * K * (Cv + 1)
+    w = (torch.randn(256, cin, 1, 1, generator=gen) * 0.05).to(DEV)
+    bias = torch.randn(256, generator=gen).to(DEV)
+    lk = ops_mod.geo_lookup(pyr, corr, disp, r)
+    ref = F.relu(F.conv2d(lk.double(), w.double(), bias.double()))
+    out = ops_mod.conv1x1_lookup(pyr, corr, disp, r, ops_mod.pack_lookup_conv(w, L, Cv, r), bias=bias, act="relu",
+                                 nsplit=nsplit)
+    close(out, ref, atol=2e-5, rtol=1e-5)
+    assert not ops_mod.range_overflowed(reset=True)
+
+
 @pytest.mark.parametrize("scale", [3e5, 1e3, 1e-4, 1e-7])
 @pytest.mark.parametrize("cfg", [24, 25, 26])
 def test_conv2d_pw_range(ops_mod, scale, cfg):
