@@ -532,8 +532,8 @@ def _tuned(ks, kd, cin, cout, B, D, H, W, cfg, nsplit):
         cfg, nsplit = (e["cfg"] if cfg < 0 else cfg), (e["nsplit"] if nsplit < 0 else nsplit)
     if _SPLIT_MAXPIX and kd == 1 and D == 1 and H * W <= _SPLIT_MAXPIX:
         nsplit = 1
-    if _SPLIT_CAP and nsplit > _SPLIT_CAP:
-        nsplit = _SPLIT_CAP
+    if _SPLIT_CAP and nsplit > _SPLIT_CAP and not (e is not None and e.get("insitu")):
+        nsplit = _SPLIT_CAP          # entries chosen end to end (tools/insitu_tune.py) are kept as they are
     return cfg, nsplit
 
 

@@ -5,7 +5,7 @@ pipelined loop other streams' kernels share the CUs, so the per-layer optimum is
 end-to-end one (e.g. the split-K cap, ops._SPLIT_CAP).  Here:
 
   1. one eager forward records every conv shape and its call count;
-  2. per shape the (cfg, nsplit <= cap) candidates are timed alone (graph-timed, like
+  2. per shape the (cfg, nsplit <= --max-split) candidates are timed alone (graph-timed, like
      tune_conv.py) and the 3 fastest kept;
   3. shapes in order of their share of the step (calls x table time), each alternative is put in
      the table, the forward re-captured as a hipGraph and replayed; kept if the step gets faster
@@ -36,6 +36,7 @@ ap.add_argument("--top", type=int, default=30, help="shapes to search, by share 
 ap.add_argument("--alts", type=int, default=3, help="alternatives per shape")
 ap.add_argument("--reps", type=int, default=12, help="graph replays per evaluation")
 ap.add_argument("--min-gain", type=float, default=0.003, help="relative step gain to keep a change")
+ap.add_argument("--max-split", type=int, default=4, help="largest split-K factor among the alternatives")
 ap.add_argument("--write", action="store_true", help="merge the result into tuning/fsmi_conv.json")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
@@ -61,7 +62,7 @@ def fn(lft, rgt):
 
 
 runner = fdist.ShardedStereo(fn, 0, 1)
-cap = ops._SPLIT_CAP or 8
+cap = a.max_split               # in-situ entries bypass ops._SPLIT_CAP (they are marked "insitu")
 
 # 1. census (eager) + warmup
 ops._TUNE = None
@@ -162,7 +163,8 @@ for n, key in enumerate(order):
     print(f"[insitu] {n + 1}/{len(order)} {key} x{counts[key]}: alternatives {alts}, step {base:.3f} ms "
           f"({(time.time() - t_start) / 60:.1f} min)", file=sys.stderr, flush=True)
     for (c, s) in alts:
-        if cur is not None and cur["cfg"] == c and min(cur["nsplit"], cap) == s:
+        eff = cur["nsplit"] if cur is None or cur.get("insitu") or not ops._SPLIT_CAP else min(cur["nsplit"], ops._SPLIT_CAP)
+        if cur is not None and cur["cfg"] == c and eff == s:
             continue
         table[key] = {"cfg": c, "nsplit": s, "us": round(best_alone, 1), "insitu": True}
         t = min(evaluate(), evaluate())
