@@ -9,17 +9,20 @@
 namespace fsmi {
 namespace {
 
-constexpr int DW_TR = 16, DW_TC = 64;   // output tile per block (rows x cols), 4 rows per thread
+constexpr int DW_TR = 16, DW_TC = 64;   // conv_1in output tile per block (rows x cols), 4 rows per thread
+// dwconv: 32 x 64 output tile, 8 rows per thread -- the (KS-1)-row halo is re-read for half as many
+// outputs and each LDS window row feeds up to 8 accumulators (16 x 64 with 4 rows: 1 TB/s at cfg2)
+constexpr int DWK_TR = 32, DWK_RPT = 8;
 
 template <int KS>
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias, float* __restrict__ out,
                                                      int C, int H, int W, int ntr, int ntc) {
-  constexpr int P = KS / 2, IR = DW_TR + KS - 1, IC = DW_TC + KS - 1;
+  constexpr int P = KS / 2, IR = DWK_TR + KS - 1, IC = DW_TC + KS - 1, RPT = DWK_RPT;
   __shared__ float tile[IR][IC + 1];
   const int plane = blockIdx.x / (ntr * ntc);
   const int t = blockIdx.x - plane * ntr * ntc;
-  const int r0 = (t / ntc) * DW_TR, c0 = (t % ntc) * DW_TC;
+  const int r0 = (t / ntc) * DWK_TR, c0 = (t % ntc) * DW_TC;
   const int c = plane % C;
   const float* xp = x + static_cast<size_t>(plane) * H * W;
   for (int e = threadIdx.x; e < IR * IC; e += 256) {
@@ -31,16 +34,18 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
 #pragma unroll
   for (int k = 0; k < KS * KS; ++k) wk[k] = w[c * KS * KS + k];   // block-uniform: scalar loads
   __syncthreads();
-  const int col = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
+  const int col = threadIdx.x & 63, rb = (threadIdx.x >> 6) * RPT;
   const float b0 = bias ? bias[c] : 0.f;
-  float acc[4] = {b0, b0, b0, b0};
+  float acc[RPT];
 #pragma unroll
-  for (int ir = 0; ir < 4 + KS - 1; ++ir) {
+  for (int o = 0; o < RPT; ++o) acc[o] = b0;
+#pragma unroll
+  for (int ir = 0; ir < RPT + KS - 1; ++ir) {
     float v[KS];
 #pragma unroll
     for (int kw = 0; kw < KS; ++kw) v[kw] = tile[rb + ir][col + kw];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
+    for (int o = 0; o < RPT; ++o) {
       const int kh = ir - o;
       if (kh >= 0 && kh < KS) {
 #pragma unroll
@@ -50,7 +55,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
   }
   float* op = out + static_cast<size_t>(plane) * H * W;
 #pragma unroll
-  for (int o = 0; o < 4; ++o) {
+  for (int o = 0; o < RPT; ++o) {
     const int hh = r0 + rb + o, ww = c0 + col;
     if (hh < H && ww < W) op[hh * W + ww] = acc[o];
   }
@@ -163,7 +168,7 @@ extern "C" int fsmi_dwconv2d(const float* x, const float* w, const float* bias, 
   FSMI_CHECK_ARG(KS == 3 || KS == 5 || KS == 7, "fsmi_dwconv2d: kernel %d unsupported (3, 5, 7)", KS);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_DWCONV, s);
-  const int ntr = (H + DW_TR - 1) / DW_TR, ntc = (W + DW_TC - 1) / DW_TC;
+  const int ntr = (H + DWK_TR - 1) / DWK_TR, ntc = (W + DW_TC - 1) / DW_TC;
   const dim3 grid(static_cast<unsigned>(B) * C * ntr * ntc);
   if (KS == 7) hipLaunchKernelGGL(dwconv_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
   else if (KS == 5) hipLaunchKernelGGL(dwconv_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
