@@ -37,6 +37,8 @@ PIPELINE = os.environ.get("FSMI_PIPELINE", "1") != "0"
 PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 
 
+# the disparity head writes disp + delta into the next encoder buffer (A/B knob)
+HEAD_INPLACE = os.environ.get("FSMI_HEAD_INPLACE", "1") != "0"
 # opt-in (A/B): the lookup fused into convc1's staging (ops.conv1x1_lookup), so the lookup tensor
 # never exists.  Parity-green but measured slower end to end (cfg2: 15.8 vs 16.6 pairs/s; the fused
 # kernel 279 us vs 169 us for lookup + convc1 alone): its gathers sit on the conv's critical path at
@@ -121,15 +123,22 @@ class DispHead(nn.Module):
             EdgeNextConvEncoder(input_dim, expan_ratio=4, kernel_size=7, norm=None),
             nn.Conv2d(input_dim, output_dim, 3, padding=1))
 
-    def forward(self, x):
+    def forward(self, x, res=None, out=None, co0=0):
+        """``res``: returns res + head(x) from the last conv's epilogue (the loop's ``disp + delta``,
+        same fp32 sum), written into channel ``co0`` of ``out`` when given (HIP path only)."""
         if not _fast(x):
-            return self.conv(x)
+            y = self.conv(x)
+            return y if res is None else res + y
         y = _conv(self.conv[0], [_f32(x)], "relu")
         for enc in (self.conv[2], self.conv[3]):
             d = ops.dwconv2d(y, enc.dwconv.weight, enc.dwconv.bias)   # depthwise 7x7; norm=None
             e = _conv(enc.pwconv1, [d], "gelu")
             y = _conv(enc.pwconv2, [e], gamma=enc.gamma, res=y)  # x + gamma * pw2(gelu(pw1(.)))
-        return _conv(self.conv[4], [y])
+        if res is not None:
+            res = res.float()
+            if not res.is_contiguous():
+                res = res.contiguous()
+        return _conv(self.conv[4], [y], res=res, out=out, co0=co0)
 
 
 class ConvGRU(nn.Module):
@@ -207,7 +216,9 @@ class BasicMotionEncoder(nn.Module):
         nc, nd = c.shape[1], d.shape[1]
         pk, b = _packed(self.conv, cin_order=tuple(range(nc, nc + nd)) + tuple(range(nc)))
         ops.conv2d([d, c], pk, bias=b, act="relu", out=out, co0=0)
-        out[:, self.conv.out_channels:].copy_(disp)
+        tail = out[:, self.conv.out_channels:]
+        if tail.data_ptr() != disp.data_ptr():        # run_pipelined has the head write it in place
+            tail.copy_(disp)
         return out
 
     def forward(self, disp, corr):
@@ -440,8 +451,16 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1))
         _BRANCH[0] = 1
         mask = None
+        # the disparity lives in the last channel of the encoder output it feeds: the disparity head
+        # writes disp + delta straight into the next iteration's buffer (no cat copy, no add pass)
+        nc = self.encoder.conv.out_channels
+        enc = disp.new_empty(B, nc + 1, H, W)                                   # on main
+        if HEAD_INPLACE:
+            enc[:, nc:].copy_(disp)
+            disp = enc[:, nc:]
         for t in range(iters):
-            enc = disp.new_empty(B, self.encoder.conv.out_channels + 1, H, W)   # on main
+            if not HEAD_INPLACE and t:
+                enc = disp.new_empty(B, nc + 1, H, W)
             s_mot.wait_stream(main)
             with torch.cuda.stream(s_mot):
                 self.encoder.motion_into(disp, geo_fn, enc)
@@ -464,9 +483,15 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             s_mot.wait_stream(main)
             with torch.cuda.stream(s_mot):
                 mask = _conv(self.mask[2], [_conv(self.mask[0], [n0], "relu")], "relu", alpha=0.25)
-            delta = self.disp_head(n0)
+            if t + 1 < iters and HEAD_INPLACE:
+                enc = disp.new_empty(B, nc + 1, H, W)
+                self.disp_head(n0, res=disp, out=enc, co0=nc)
+                disp = enc[:, nc:]
+            elif HEAD_INPLACE:
+                disp = self.disp_head(n0, res=disp)
+            else:
+                disp = disp + self.disp_head(n0).float()
             main.wait_stream(s_mot)
-            disp = disp + delta.float()
         main.wait_stream(s_gru)
         return [n0, n1, n2], mask, disp
 
