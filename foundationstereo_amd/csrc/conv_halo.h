@@ -98,6 +98,11 @@ struct HaloArgs {
   float* grh;                      // sigmoid(r_pre) * h, written by act 3
   int gHd;
   int* ovf;                        // range flag (host-mapped; set to 1 when a scaled value overflows fp16)
+  // transposed-conv phase launches (fsmi_conv3d_up2_halo_x3; all 0 otherwise): the input window
+  // shifted by (sd, sh, sw) in {0, 1}, and output voxel (d, h, w) written at (2d + od, 2h + oh,
+  // 2w + ow) of the (2D, 2H, 2W) output, whose channel stride is ocstride
+  int up, sd, sh, sw, od, oh, ow;
+  long long ocstride;
 };
 
 // Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
@@ -208,6 +213,7 @@ __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, f
                                            const float* __restrict__ gh, float* __restrict__ gz,
                                            const float* __restrict__ gatt, float* __restrict__ grh) {
   const long long HW = a.cstride;
+  const long long OHW = RESPRE && a.up ? a.ocstride : HW;   // output channel stride (transposed conv)
   float2 q[16];                    // (weight scale 2^-wexp[co], bias[co]) of the 16 rows
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -251,7 +257,7 @@ __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, f
       else if constexpr (ACT == 2) x = gelu_erf_h(x);
       else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
       if (!pre) x = x * a.alpha * gv[r] + rv;
-      out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw] = x;
+      out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * OHW + hw] = x;
     }
   }
 }
@@ -285,7 +291,7 @@ struct HaloStage {
       const int task = min(tid + 256 * u, X_TASKS - 1);
       const int hp = task % NHP, g = task / NHP;
       const int hr = hp / HC, hc = hp - hr * HC;
-      const int hh = r0 + hr - PD, ww = c0 + hc - PD;
+      const int hh = r0 + hr - PD + a.sh, ww = c0 + hc - PD + a.sw;
       const bool in = hh >= 0 && hh < a.H && ww >= 0 && ww < a.W && tid + 256 * u < X_TASKS;
       const int pix = min(max(hh, 0), a.H - 1) * a.W + min(max(ww, 0), a.W - 1);
       desc[u] = (pix << 3) | (in ? 4 : 0) | g;
@@ -510,7 +516,9 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
   for (int j = 0; j < TN; ++j) {
     const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
     if (hh >= a.H || ww >= a.W) continue;
-    const long long hw = static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
+    const long long hw = D3 && a.up ? (static_cast<long long>(2 * t.d0 + a.od) * 2 * a.H + 2 * hh + a.oh) * 2 * a.W
+                                          + 2 * ww + a.ow
+                                    : static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
       if ((fown >> (i * TN + j)) & 1u)
@@ -637,7 +645,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   const int cc_end = min(nq, cc_begin + a.kpc);
   int step = 0;
   load_w(cc_begin, 0);
-  if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD);
+  if constexpr (D3) hs.load(a, tc.b, cc_begin % nck, tc.d0 + cc_begin / nck - a.PDD + a.sd);
   else hs.load(a, tc.b, cc_begin);
   int sx = kNoExp;                 // block exponent of the split (see chunk_exp)
   bool ovf = false;
@@ -687,7 +695,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
     }
     hs.template store<RM>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
     if (cc + 1 < cc_end) {
-      if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD);
+      if constexpr (D3) hs.load(a, tc.b, (cc + 1) % nck, tc.d0 + (cc + 1) / nck - a.PDD + a.sd);
       else hs.load(a, tc.b, cc + 1);
     }   // in flight during this chunk's taps
 #pragma unroll 1
@@ -794,7 +802,8 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
 
     // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
     auto chunk = [&](auto par_c, int cc) FSMI_HALO_INL {
-      constexpr int P = decltype(par_c)::value;
+      // an even tap count (KS = 2) starts every chunk on buffer 0; an odd one alternates
+      constexpr int P = (NTAP & 1) ? decltype(par_c)::value : 0;
 #pragma unroll
       for (int tap = 0; tap < NTAP; ++tap) {
         const bool last = tap + 1 == NTAP;
@@ -857,7 +866,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
         }
         hs.template store<RM>(gXh, gXl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
         if (cc + KG < cc_end && !(a.dbg & 2)) {
-          if constexpr (D3) hs.load(a, tc.b, (cc + KG) % nck, tc.d0 + (cc + KG) / nck - a.PDD);
+          if constexpr (D3) hs.load(a, tc.b, (cc + KG) % nck, tc.d0 + (cc + KG) / nck - a.PDD + a.sd);
           else hs.load(a, tc.b, cc + KG);
         }   // in flight during this chunk's taps
       }
@@ -865,7 +874,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
     };
     if (n_g > 0) {
       load_wf(std::integral_constant<int, 0>(), c_first, 0);
-      if constexpr (D3) hs.load(a, tc.b, c_first % nck, tc.d0 + c_first / nck - a.PDD);
+      if constexpr (D3) hs.load(a, tc.b, c_first % nck, tc.d0 + c_first / nck - a.PDD + a.sd);
       else hs.load(a, tc.b, c_first);
     }
     // chunks in pairs so every register-buffer index is static (parity 0, then 1)

@@ -105,8 +105,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(scale_bias) % 8 == 0, "%s: scale_bias must be 8-B aligned", what);
   FSMI_CHECK_ARG(nseg >= 1 && nseg <= kHMaxSeg, "%s: 1..%d segments, got %d", what, kHMaxSeg, nseg);
   FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "%s: bad shape", what);
-  FSMI_CHECK_ARG(KS == 1 || KS == 3, "%s: kernel %d unsupported (1, 3)", what, KS);
-  FSMI_CHECK_ARG(D >= 1 && KD >= 1 && KD % 2 == 1, "%s: depth %d / depth kernel %d (odd)", what, D, KD);
+  FSMI_CHECK_ARG(KS == 1 || KS == 3 || (KS == 2 && a.up && KD == 2), "%s: kernel %d unsupported (1, 3)", what, KS);
+  FSMI_CHECK_ARG(D >= 1 && KD >= 1 && (KD % 2 == 1 || a.up), "%s: depth %d / depth kernel %d (odd)", what, D, KD);
   FSMI_CHECK_ARG(a.act == 3 || (out && co0 >= 0 && co0 + Cout <= out_ctot), "%s: output slice outside the tensor",
                  what);
   int cin = 0;
@@ -212,7 +212,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     return e ? std::atoi(e) : 0;
   }();
   a.dbg = conv_dbg;
-  const int rc = pw ? halo::launch_pw(cfg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
+  const int rc = pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
   if (a.nsplit > 1) halo::split_reduce(a, s);
@@ -283,4 +283,38 @@ extern "C" int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, con
   const int ch[1] = {Cin}, tot[1] = {Cin};
   return run_halo(a, "fsmi_conv3d_halo_x3", seg, ch, tot, 1, whi, wlo, scale_bias, out, Cout, 0, B, Cout, KS, H, W,
                   cfg, nsplit, ws, ws_floats, stream, D, KD);
+}
+
+extern "C" int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* const* whi, const void* const* wlo,
+                                       const float* const* scale_bias, float* out, int B, int Cout, int D, int H,
+                                       int W, int act, int cfg, void* stream) {
+  FSMI_CHECK_ARG(x && out && whi && wlo && scale_bias && Cin > 0, "fsmi_conv3d_up2_halo_x3: null pointer / channels");
+  FSMI_CHECK_ARG(act == 0 || act == 1 || act == 6, "fsmi_conv3d_up2_halo_x3: act %d (0, 1, 6)", act);
+  if (cfg < 0) cfg = Cout <= 32 ? 7 : (Cout <= 64 ? 5 : 3);
+  FSMI_CHECK_ARG(cfg == 2 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7,
+                 "fsmi_conv3d_up2_halo_x3: tile %d (2, 3, 5, 6, 7)", cfg);
+  const long long V = static_cast<long long>(D) * H * W;
+  for (int p = 0; p < 8; ++p) {
+    const int pd = p >> 2, ph = (p >> 1) & 1, pw = p & 1;
+    FSMI_CHECK_ARG(whi[p] && wlo[p] && scale_bias[p], "fsmi_conv3d_up2_halo_x3: null phase %d", p);
+    HaloArgs a{};
+    a.act = act;
+    a.alpha = 1.f;
+    a.up = 1;
+    a.sd = pd;
+    a.sh = ph;
+    a.sw = pw;
+    a.od = pd;
+    a.oh = ph;
+    a.ow = pw;
+    a.ocstride = 8 * V;
+    const float* seg[1] = {x};
+    const int ch[1] = {Cin}, tot[1] = {Cin};
+    // out_ctot = 8 * Cout: run_halo's batch stride (out_ctot x the input volume) is then the
+    // (Cout, 2D, 2H, 2W) output's
+    const int rc = run_halo(a, "fsmi_conv3d_up2_halo_x3", seg, ch, tot, 1, whi[p], wlo[p], scale_bias[p], out,
+                            8 * Cout, 0, B, Cout, 2, H, W, cfg, 1, nullptr, 0, stream, D, 2);
+    if (rc != FSMI_OK) return rc;
+  }
+  return FSMI_OK;
 }

@@ -301,7 +301,7 @@ class PackedConv:
         assert self.k == kw
         self.mode = mode
         assert mode in ("f32", "x3", "halo"), mode
-        assert mode != "halo" or self.k in (1, 3), "halo conv: 1x1 or 3x3 only"
+        assert mode != "halo" or self.k in (1, 2, 3), "halo conv: 1x1, 2x2 (transposed-conv phases) or 3x3"
         assert self.kd == 1 or mode == "halo", "3D weights: halo mode only"
         if mode == "f32":
             self.wpk = pack_conv_weight(w[..., 0])
@@ -389,6 +389,51 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
         _p(x), Cin, _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
         _p(res) if res is not None else None, _p(out), B, pk.cout, D, H, W, pk.kd, pk.k, _ACT3D[act],
         1 if res_pre else 0, cfg, nsplit, _p(ws), ws.numel(), stream), "conv3d")
+    return out
+
+
+# kernel index of each 2-tap phase conv of ConvTranspose3d(k=4, s=2, p=1): output 2m + p reads input
+# m - 1 + t (+1 for p = 1) through kernel element _UP2_K[p][t]
+_UP2_K = ((3, 1), (2, 0))
+
+
+def pack_deconv_phases(weight: Tensor, scale: Tensor = None):
+    """ConvTranspose3d(k=4, s=2, p=1) weight (Cin, Cout, 4, 4, 4), optionally scaled per output
+    channel (folded BatchNorm), as the 8 phase convs of ``fsmi_conv3d_up2_halo_x3``."""
+    w = weight.detach().double()
+    assert w.dim() == 5 and tuple(w.shape[2:]) == (4, 4, 4), "pack_deconv_phases: k = 4 only"
+    if scale is not None:
+        w = w * scale.detach().double().view(1, -1, 1, 1, 1)
+    packs = []
+    for p in range(8):
+        pd, ph, pw = p >> 2, (p >> 1) & 1, p & 1
+        kd = [_UP2_K[pd][t] for t in range(2)]
+        kh = [_UP2_K[ph][t] for t in range(2)]
+        kw = [_UP2_K[pw][t] for t in range(2)]
+        wp = w[:, :, kd][:, :, :, kh][:, :, :, :, kw]            # (Cin, Cout, 2, 2, 2)
+        packs.append(PackedConv(wp.permute(1, 0, 2, 3, 4).float().contiguous(), mode="halo"))
+    return packs
+
+
+def conv3d_up2(x: Tensor, packs, bias: Tensor = None, act=None, cfg: int = -1) -> Tensor:
+    """ConvTranspose3d(k=4, s=2, p=1) (+ bias / folded BN, activation) on the halo kernel's 2x2x2
+    phase tiles: (B, Cin, D, H, W) -> (B, Cout, 2D, 2H, 2W)."""
+    assert len(packs) == 8 and all(pk.mode == "halo" and pk.k == 2 and pk.kd == 2 for pk in packs)
+    _check("conv3d_up2", x, *([bias] if bias is not None else []))
+    B, Cin, D, H, W = x.shape
+    pk0 = packs[0]
+    assert Cin == pk0.cin, f"conv3d_up2: {Cin} input channels for a conv packed with {pk0.cin}"
+    x = _c(x)
+    out = torch.empty((B, pk0.cout, 2 * D, 2 * H, 2 * W), device=x.device, dtype=torch.float32)
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * Cin * pk0.cout * 64 * B * D * H * W
+    whi, k1 = _lib.ptr_array([_p(pk.whi) for pk in packs])
+    wlo, k2 = _lib.ptr_array([_p(pk.wlo) for pk in packs])
+    sbs = [pk.scale_bias(bias) for pk in packs]
+    sb, k3 = _lib.ptr_array([_p(t) for t in sbs])
+    _lib.check(_lib.load().fsmi_conv3d_up2_halo_x3(_p(x), Cin, whi, wlo, sb, _p(out), B, pk0.cout, D, H, W,
+                                                   _ACT3D[act], cfg, _stream(x)), "conv3d_up2")
+    del k1, k2, k3
     return out
 
 

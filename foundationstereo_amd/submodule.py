@@ -51,6 +51,8 @@ class LayerNorm2d(nn.LayerNorm):
 
 
 FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
+# A/B knob: the hourglass ConvTranspose3d *_up on the halo kernel's 2x2x2 phase tiles
+UP3D = os.environ.get("FSMI_UP3D", "0") == "1"
 DT_FAST = os.environ.get("FSMI_DT", "1") != "0"      # disparity transformer on csrc/transformer.hip
 
 
@@ -76,6 +78,40 @@ def _fast3d(x, conv, bn) -> bool:
         return False
     return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm3d and not bn.training
                                                          and bn.track_running_stats)
+
+
+def _fast_up3d(x, conv, bn) -> bool:
+    """ConvTranspose3d(k=4, s=2, p=1) (+ eval BatchNorm3d) that the 2x2x2 phase tiles run."""
+    if not (FILTER3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+            and type(conv) is nn.ConvTranspose3d):
+        return False
+    if conv.kernel_size != (4, 4, 4) or conv.stride != (2, 2, 2) or conv.padding != (1, 1, 1) \
+            or conv.output_padding != (0, 0, 0) or conv.dilation != (1, 1, 1) or conv.groups != 1:
+        return False
+    return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm3d and not bn.training
+                                                         and bn.track_running_stats)
+
+
+def _packed_up(conv, bn):
+    """The 8 phase packs of a ConvTranspose3d with its eval BatchNorm folded (fp64 fold), cached."""
+    ts = [conv.weight] + ([conv.bias] if conv.bias is not None else [])
+    is_bn = isinstance(bn, nn.BatchNorm3d)
+    if is_bn:
+        ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    key = tuple((t.data_ptr(), t._version) for t in ts)
+    hit = conv.__dict__.get("_fsmi_pack_up")
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            cout = conv.weight.shape[1]
+            b = conv.bias.detach().double() if conv.bias is not None else torch.zeros(
+                cout, dtype=torch.float64, device=conv.weight.device)
+            sc = None
+            if is_bn:
+                sc = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+                b = (b - bn.running_mean.double()) * sc + bn.bias.double()
+            hit = (key, ops.pack_deconv_phases(conv.weight, sc), b.float().contiguous())
+        conv.__dict__["_fsmi_pack_up"] = hit
+    return hit[1], hit[2]
 
 
 def _fast2d(x, conv, bn) -> bool:
@@ -152,6 +188,9 @@ class BasicConv(nn.Module):
         bn = self.bn if self.use_bn else None
         if _fast3d(x, self.conv, bn):        # stride-1 3D conv + folded BN + LeakyReLU, one kernel
             return conv3d_bn_act(x, self.conv, bn, "leaky" if self.relu else None)
+        if UP3D and _fast_up3d(x, self.conv, bn):   # ConvTranspose3d k4 s2: 8 phase convs, BN folded
+            packs, b = _packed_up(self.conv, bn)
+            return ops.conv3d_up2(_f32(x), packs, bias=b, act="leaky" if self.relu else None)
         if _fast2d(x, self.conv, bn):
             return conv2d_bn_act([x], self.conv, bn, "leaky" if self.relu else None)
         x = self.bn(self.conv(x)) if self.use_bn else self.conv(x)

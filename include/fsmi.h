@@ -248,6 +248,18 @@ int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wl
  *   dwconv of DispHead (core/submodule.py:565-591 via core/update.py:24-31).
  * fsmi_resize_bilinear: F.interpolate(x, (Ho,Wo), mode="bilinear",
  *   align_corners=True) on (B,C,Hi,Wi) -> (B,C,Ho,Wo) (interp, core/update.py:80). */
+/* ---- a3: ConvTranspose3d(k=4, s=2, p=1) + folded BatchNorm + activation -------------
+ * replaces the hourglass *_up BasicConv(deconv=True, is_3d=True), core/foundation_stereo.py:62-68
+ * with core/submodule.py:51-86: x (B,Cin,D,H,W) -> out (B,Cout,2D,2H,2W).  Output phase
+ * p = 4*pd + 2*ph + pw (voxels (2d+pd, 2h+ph, 2w+pw)) is a 2x2x2 stride-1 conv over x:
+ * whi[p] / wlo[p] packed as fsmi_conv3d_halo_x3's weights (KD = KS = 2, taps at input offsets
+ * {-1, 0} for phase 0 and {0, +1} for phase 1 of each dimension; ops.pack_deconv_phases),
+ * scale_bias[p] its (2^-wexp, bias) pairs.  act 0 none / 1 ReLU / 6 LeakyReLU(0.01); cfg tile
+ * (2, 3, 5, 6, 7) or -1. */
+int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* const* whi, const void* const* wlo,
+                            const float* const* scale_bias, float* out, int B, int Cout, int D, int H, int W,
+                            int act, int cfg, void* stream);
+
 int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
                   int H, int W, void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);

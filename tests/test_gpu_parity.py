@@ -230,6 +230,27 @@ def test_conv2d_pw_vs_torch(ops_mod, cfg, cout, act, wide, nsplit, HW):
     assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
 
 
+@pytest.mark.parametrize("cfg", [-1, 2, 3, 5, 6, 7])
+@pytest.mark.parametrize("cin,cout,D,H,W,B", [(56, 28, 6, 9, 37, 1), (112, 56, 3, 8, 20, 2), (168, 112, 2, 4, 10, 1)])
+def test_conv3d_up2_vs_torch(ops_mod, cin, cout, D, H, W, B, cfg):
+    """ConvTranspose3d(k=4, s=2, p=1) + folded eval BatchNorm + LeakyReLU (the hourglass *_up,
+    core/foundation_stereo.py:62-68) as 8 phase convs on the 2x2x2 halo tiles vs fp64 torch: ragged
+    row / column / cout tiles, multi-chunk Cin, batch 2."""
+    import torch.nn.functional as F
+    gen = torch.Generator().manual_seed(cin + cout + D)
+    x = torch.randn(B, cin, D, H, W, generator=gen)
+    w = torch.randn(cin, cout, 4, 4, 4, generator=gen) * 0.05
+    sc = torch.rand(cout, generator=gen) + 0.5
+    sh = torch.randn(cout, generator=gen) * 0.1
+    packs = ops_mod.pack_deconv_phases(g(w), g(sc))
+    out = ops_mod.conv3d_up2(g(x), packs, bias=g(sh), act="leaky", cfg=cfg)
+    ref = F.conv_transpose3d(x.double(), w.double(), stride=2, padding=1) * sc.double().view(1, -1, 1, 1, 1) \
+        + sh.double().view(1, -1, 1, 1, 1)
+    ref = F.leaky_relu(ref, 0.01)
+    assert out.shape == ref.shape
+    close(out, ref, atol=2e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("L,Cv,D,H,W,B,nsplit", [(4, 28, 48, 12, 40, 1, 1), (2, 8, 24, 5, 37, 2, 2),
                                                    (4, 28, 48, 30, 40, 1, 3), (3, 28, 80, 7, 64, 1, 2)])
 def test_conv1x1_lookup_vs_unfused(ops_mod, L, Cv, D, H, W, B, nsplit):
