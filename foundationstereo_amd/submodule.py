@@ -51,8 +51,12 @@ class LayerNorm2d(nn.LayerNorm):
 
 
 FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
-# A/B knob: the hourglass ConvTranspose3d *_up on the halo kernel's 2x2x2 phase tiles
-UP3D = os.environ.get("FSMI_UP3D", "0") == "1"
+# The hourglass ConvTranspose3d *_up on the halo kernel's 2x2x2 phase tiles for inputs of at least
+# UP3D_MINVOX voxels.  The 8 phase launches of a small volume leave most CUs idle: at cfg2
+# (tools/up3d_bench.py) conv1_up (56->28 from 24x60x80) runs 379 us vs 714 us for MIOpen/CK + BN +
+# LeakyReLU, conv2_up (12x30x40) 284 vs 256 us, conv3_up (6x15x20) 276 vs 101 us.
+UP3D = os.environ.get("FSMI_UP3D", "1") != "0"
+UP3D_MINVOX = int(os.environ.get("FSMI_UP3D_MINVOX", "32768"))
 DT_FAST = os.environ.get("FSMI_DT", "1") != "0"      # disparity transformer on csrc/transformer.hip
 
 
@@ -87,6 +91,8 @@ def _fast_up3d(x, conv, bn) -> bool:
         return False
     if conv.kernel_size != (4, 4, 4) or conv.stride != (2, 2, 2) or conv.padding != (1, 1, 1) \
             or conv.output_padding != (0, 0, 0) or conv.dilation != (1, 1, 1) or conv.groups != 1:
+        return False
+    if x.shape[2] * x.shape[3] * x.shape[4] < UP3D_MINVOX:
         return False
     return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm3d and not bn.training
                                                          and bn.track_running_stats)
