@@ -103,6 +103,10 @@ struct HaloArgs {
   // 2w + ow) of the (2D, 2H, 2W) output, whose channel stride is ocstride
   int up, sd, sh, sw, od, oh, ow;
   long long ocstride;
+  // up == 2: all eight phases in one launch (blocks phase-major), phase p's weights / scale-bias
+  const _Float16* whi8[8];
+  const _Float16* wlo8[8];
+  const float2* sb8[8];
 };
 
 // Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
@@ -484,8 +488,8 @@ __device__ __forceinline__ TileCoord tile_coord(const HaloArgs& a, int ctile, in
 
 // cout-tile-major logical order over an XCD-aware remap: an XCD's blocks share weights in its L2
 template <int BM, int TR, bool D3>
-__device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a) {
-  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+__device__ __forceinline__ TileCoord decode_tile(const HaloArgs& a, unsigned bid, unsigned nblocks) {
+  const unsigned item = xcd_remap(bid, nblocks);
   const int cs = item / a.npix;                    // (cout tile, split) pair
   const int ptile = item - cs * a.npix;
   const int ctile = cs / a.nsplit;
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int hsel = lane >> 5, rl = lane & 31;
-  const TileCoord tc = decode_tile<BM, TR, D3>(a);
+  const TileCoord tc = decode_tile<BM, TR, D3>(a, blockIdx.x, gridDim.x);
   const int m0 = tc.m0;
   const int nck = a.CinP / HKC;
   const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
@@ -934,14 +938,34 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
     }
   };
 
-  const TileCoord tc = decode_tile<BM, TR, D3>(a);
+  unsigned bid = blockIdx.x, nb = gridDim.x;
+  if constexpr (KS == 2) {
+    if (a.up == 2) {                               // transposed-conv phases, phase-major blocks
+      nb /= 8;
+      const int ph = static_cast<int>(bid / nb);
+      bid -= static_cast<unsigned>(ph) * nb;
+      // constant indices only (a dynamic index into the by-value args puts them in scratch)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (ph == q) {
+          a.whi = a.whi8[q];
+          a.wlo = a.wlo8[q];
+          a.sb = a.sb8[q];
+        }
+      }
+      a.sd = a.od = ph >> 2;
+      a.sh = a.oh = (ph >> 1) & 1;
+      a.sw = a.ow = ph & 1;
+    }
+  }
+  const TileCoord tc = decode_tile<BM, TR, D3>(a, bid, nb);
   const int c0 = tc.split * a.kpc;
   segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
 }
 
 template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1>
 void launch_tile(const HaloArgs& a, hipStream_t s) {
-  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit;
+  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit * (a.up == 2 ? 8 : 1);
   if constexpr (WREG)
     hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3, KG>), dim3(grid), dim3(256 * KG), 0, s, a);
   else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);

@@ -290,31 +290,31 @@ extern "C" int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* cons
                                        int W, int act, int cfg, void* stream) {
   FSMI_CHECK_ARG(x && out && whi && wlo && scale_bias && Cin > 0, "fsmi_conv3d_up2_halo_x3: null pointer / channels");
   FSMI_CHECK_ARG(act == 0 || act == 1 || act == 6, "fsmi_conv3d_up2_halo_x3: act %d (0, 1, 6)", act);
-  if (cfg < 0) cfg = Cout <= 32 ? 7 : (Cout <= 64 ? 5 : 3);
+  // tools/up3d_bench.py at cfg2 (one launch, 8 phases): 32-cout x 4-row tiles for 28 and 112 couts,
+  // 64 x 8 for 56 (conv1_up 296 us, conv2_up 139 us, conv3_up 64 us vs 711 / 249 / 97 us for
+  // MIOpen / CK + BatchNorm + LeakyReLU)
+  if (cfg < 0) cfg = (Cout > 32 && Cout <= 64) ? 2 : 7;
   FSMI_CHECK_ARG(cfg == 2 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7,
                  "fsmi_conv3d_up2_halo_x3: tile %d (2, 3, 5, 6, 7)", cfg);
   const long long V = static_cast<long long>(D) * H * W;
+  HaloArgs a{};
   for (int p = 0; p < 8; ++p) {
-    const int pd = p >> 2, ph = (p >> 1) & 1, pw = p & 1;
     FSMI_CHECK_ARG(whi[p] && wlo[p] && scale_bias[p], "fsmi_conv3d_up2_halo_x3: null phase %d", p);
-    HaloArgs a{};
-    a.act = act;
-    a.alpha = 1.f;
-    a.up = 1;
-    a.sd = pd;
-    a.sh = ph;
-    a.sw = pw;
-    a.od = pd;
-    a.oh = ph;
-    a.ow = pw;
-    a.ocstride = 8 * V;
-    const float* seg[1] = {x};
-    const int ch[1] = {Cin}, tot[1] = {Cin};
-    // out_ctot = 8 * Cout: run_halo's batch stride (out_ctot x the input volume) is then the
-    // (Cout, 2D, 2H, 2W) output's
-    const int rc = run_halo(a, "fsmi_conv3d_up2_halo_x3", seg, ch, tot, 1, whi[p], wlo[p], scale_bias[p], out,
-                            8 * Cout, 0, B, Cout, 2, H, W, cfg, 1, nullptr, 0, stream, D, 2);
-    if (rc != FSMI_OK) return rc;
+    FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(scale_bias[p]) % 8 == 0, "fsmi_conv3d_up2_halo_x3: scale_bias align");
+    a.whi8[p] = static_cast<const _Float16*>(whi[p]);
+    a.wlo8[p] = static_cast<const _Float16*>(wlo[p]);
+    a.sb8[p] = reinterpret_cast<const float2*>(scale_bias[p]);
   }
+  a.act = act;
+  a.alpha = 1.f;
+  a.up = 2;                                       // all eight phases in one launch
+  a.ocstride = 8 * V;
+  const float* seg[1] = {x};
+  const int ch[1] = {Cin}, tot[1] = {Cin};
+  // out_ctot = 8 * Cout: run_halo's batch stride (out_ctot x the input volume) is then the
+  // (Cout, 2D, 2H, 2W) output's
+  const int rc = run_halo(a, "fsmi_conv3d_up2_halo_x3", seg, ch, tot, 1, whi[0], wlo[0], scale_bias[0], out,
+                          8 * Cout, 0, B, Cout, 2, H, W, cfg, 1, nullptr, 0, stream, D, 2);
+  if (rc != FSMI_OK) return rc;
   return FSMI_OK;
 }

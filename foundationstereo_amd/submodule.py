@@ -51,12 +51,12 @@ class LayerNorm2d(nn.LayerNorm):
 
 
 FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
-# The hourglass ConvTranspose3d *_up on the halo kernel's 2x2x2 phase tiles for inputs of at least
-# UP3D_MINVOX voxels.  The 8 phase launches of a small volume leave most CUs idle: at cfg2
-# (tools/up3d_bench.py) conv1_up (56->28 from 24x60x80) runs 379 us vs 714 us for MIOpen/CK + BN +
-# LeakyReLU, conv2_up (12x30x40) 284 vs 256 us, conv3_up (6x15x20) 276 vs 101 us.
+# The hourglass ConvTranspose3d *_up on the halo kernel's 2x2x2 phase tiles (all 8 output phases in
+# one launch; tools/up3d_bench.py at cfg2: conv1_up 296 us, conv2_up 139 us, conv3_up 64 us vs
+# 711 / 249 / 97 us for MIOpen / CK + BatchNorm + LeakyReLU).  UP3D_MINVOX: smallest input volume
+# sent there (A/B knob).
 UP3D = os.environ.get("FSMI_UP3D", "1") != "0"
-UP3D_MINVOX = int(os.environ.get("FSMI_UP3D_MINVOX", "32768"))
+UP3D_MINVOX = int(os.environ.get("FSMI_UP3D_MINVOX", "0"))
 DT_FAST = os.environ.get("FSMI_DT", "1") != "0"      # disparity transformer on csrc/transformer.hip
 
 
