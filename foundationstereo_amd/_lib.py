@@ -48,6 +48,8 @@ SIGNATURES = {
                                  _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, ctypes.c_longlong, _P],
     "fsmi_conv3d_halo_x3": [_P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P,
                             ctypes.c_longlong, _P],
+    "fsmi_conv3d_halo_x3_ex": [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
+                               _P, ctypes.c_longlong, _P],
     "fsmi_conv3d_up2_halo_x3": [_P, _I, _PP, _PP, _PP, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],

@@ -107,6 +107,15 @@ struct HaloArgs {
   const _Float16* whi8[8];
   const _Float16* wlo8[8];
   const float2* sb8[8];
+  // stride-2 volume launches (fsmi_conv3d_s2_halo_x3; str = 1 otherwise): D, H, W, cstride above are
+  // the OUTPUT's, the input is (iD, iH, iW) with channel stride icstride; output voxel (d, h, w)
+  // reads input (2d + kd - 1, 2h + kh - 1, 2w + kw - 1)
+  int str, iD, iH, iW;
+  long long icstride;
+  // FeatureAtt gate (core/submodule.py:438-454) fused into a volume conv's epilogue: the final
+  // value of output channel co at (d, h, w) is multiplied by sigmoid(fatt[b, co, h, w]),
+  // fatt (B, Cout, H, W) contiguous; nullptr: no gate
+  const float* fatt;
 };
 
 // Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
@@ -117,6 +126,8 @@ int launch_cfg(int cfg, int kg, const HaloArgs& a, hipStream_t s);
 // Pointwise tiles (cfg 24-26, conv_pw.hip): 1x1 2D layers with an LDS-DMA input ring.
 // pw_tile sets the tile geometry (a.nct = pixel tiles per image, npix, nco) before split-K.
 int launch_pw(int cfg, const HaloArgs& a, hipStream_t s);
+// stride-2 3x3x3 volume tiles (conv_halo_s2_3d.hip, fsmi_conv3d_s2_halo_x3)
+int launch_s2(int cfg, const HaloArgs& a, hipStream_t s);
 // split-K reduce pass over a.ws (conv_halo_x3.hip)
 void split_reduce(const HaloArgs& a, hipStream_t s);
 void pw_tile(int cfg, HaloArgs& a);
@@ -186,9 +197,15 @@ __device__ __forceinline__ void store_el(const HaloArgs& a, float v, int co, int
     return;
   }
   float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+  // FeatureAtt gate of volume convs: sigmoid(fatt[b, co, h, w]) (1 without one)
+  float g = 1.f;
+  if (RESPRE && a.fatt) {
+    const long long P = static_cast<long long>(a.H) * a.W;
+    g = sigm_h(a.fatt[(static_cast<long long>(b) * a.Cout + co) * P + hw % P]);
+  }
   if (RESPRE && a.res_pre) {       // ResNet tail: act(v + bias + res)
     v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
-    *o = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v);
+    *o = g * (a.act == 1 ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v));
     return;
   }
   if (a.act == 1) v = fmaxf(v, 0.f);
@@ -197,7 +214,7 @@ __device__ __forceinline__ void store_el(const HaloArgs& a, float v, int co, int
   v *= a.alpha;
   if (gamma) v *= gamma[co];
   if (res) v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
-  *o = v;
+  *o = g * v;
 }
 
 template <bool RESPRE = true>
@@ -212,7 +229,7 @@ __device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, in
 // block's lifetime went to the epilogue on the nsplit = 1 layers, tools/conv_phases.py.)
 template <int ACT, bool RESPRE>
 __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, float xinv, int cb, int b,
-                                           long long hw, float* __restrict__ out, const float2* __restrict__ sb,
+                                           long long hw, int hw2, float* __restrict__ out, const float2* __restrict__ sb,
                                            const float* __restrict__ gamma, const float* __restrict__ res,
                                            const float* __restrict__ gh, float* __restrict__ gz,
                                            const float* __restrict__ gatt, float* __restrict__ grh) {
@@ -250,6 +267,9 @@ __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, f
 #pragma unroll
     for (int r = 0; r < 16; ++r) gv[r] = gamma ? gamma[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)] : 1.f;
     const bool pre = RESPRE && a.res_pre;
+    // FeatureAtt gate (volumes only): sigmoid(fatt[b, co, hw2]), hw2 = h * W + w of the output plane
+    const float* __restrict__ fatt = RESPRE ? a.fatt : nullptr;
+    const long long P = static_cast<long long>(a.H) * a.W;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = cb + (r & 3) + 8 * (r >> 2);
@@ -261,6 +281,7 @@ __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, f
       else if constexpr (ACT == 2) x = gelu_erf_h(x);
       else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
       if (!pre) x = x * a.alpha * gv[r] + rv;
+      if (fatt) x *= sigm_h(fatt[(static_cast<long long>(b) * a.Cout + co) * P + hw2]);
       out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * OHW + hw] = x;
     }
   }
@@ -282,9 +303,10 @@ __device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], i
 // group); per task a packed descriptor (clamped pixel offset << 3 | in-image << 2
 // | group) computed once per block; a chunk is loaded into registers one chunk
 // ahead and split into fp16 hi/lo when stored to LDS.
-template <int KS, int TR>
+template <int KS, int TR, int STR = 1>
 struct HaloStage {
-  static constexpr int PD = KS / 2, HR = TR + KS - 1, HC = 32 + KS - 1, NHP = HR * HC;
+  // STR = 2: a stride-2 conv's window, (2 TR + 1) x 65 input pixels for TR x 32 outputs
+  static constexpr int PD = KS / 2, HR = STR * (TR - 1) + KS, HC = STR * 31 + KS, NHP = HR * HC;
   static constexpr int X_TASKS = NHP * (HKC / 8), X_PER_T = (X_TASKS + 255) / 256;
   int desc[X_PER_T];
   f32x8 xv[X_PER_T];
@@ -295,19 +317,22 @@ struct HaloStage {
       const int task = min(tid + 256 * u, X_TASKS - 1);
       const int hp = task % NHP, g = task / NHP;
       const int hr = hp / HC, hc = hp - hr * HC;
-      const int hh = r0 + hr - PD + a.sh, ww = c0 + hc - PD + a.sw;
-      const bool in = hh >= 0 && hh < a.H && ww >= 0 && ww < a.W && tid + 256 * u < X_TASKS;
-      const int pix = min(max(hh, 0), a.H - 1) * a.W + min(max(ww, 0), a.W - 1);
+      const int IH = STR == 1 ? a.H : a.iH, IW = STR == 1 ? a.W : a.iW;   // input plane
+      const int hh = STR * r0 + hr - PD + a.sh, ww = STR * c0 + hc - PD + a.sw;
+      const bool in = hh >= 0 && hh < IH && ww >= 0 && ww < IW && tid + 256 * u < X_TASKS;
+      const int pix = min(max(hh, 0), IH - 1) * IW + min(max(ww, 0), IW - 1);
       desc[u] = (pix << 3) | (in ? 4 : 0) | g;
     }
   }
 
-  // chunk cc of depth plane d (zeros outside [0, D))
+  // chunk cc of input depth plane d (zeros outside [0, D))
   __device__ __forceinline__ void load(const HaloArgs& a, int b, int cc, int d = 0) {
-    const long long HW = a.cstride;
+    const long long HW = STR == 1 ? a.cstride : a.icstride;
+    const int ID = STR == 1 ? a.D : a.iD;
     const bool full = (cc + 1) * HKC <= a.Cin;     // block-uniform: only the last chunk is ragged
-    const bool plane_ok = d >= 0 && d < a.D;
-    const long long poff = static_cast<long long>(min(max(d, 0), a.D - 1)) * a.H * a.W;
+    const bool plane_ok = d >= 0 && d < ID;
+    const long long poff = static_cast<long long>(min(max(d, 0), ID - 1)) *
+                           (STR == 1 ? a.H * a.W : a.iH * a.iW);
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u) {
       const int g = desc[u] & 3, pix = desc[u] >> 3;
@@ -526,8 +551,8 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
 #pragma unroll
     for (int i = 0; i < TM; ++i)
       if ((fown >> (i * TN + j)) & 1u)
-      store_frag<ACT, D3>(a, acc[i][j], xinv, t.m0 + (wm * TM + i) * 32 + 4 * hsel, t.b, hw, a.out, a.sb, a.gamma,
-                          a.res, a.gh, a.gz, a.gatt, a.grh);
+      store_frag<ACT, D3>(a, acc[i][j], xinv, t.m0 + (wm * TM + i) * 32 + 4 * hsel, t.b, hw, hh * a.W + ww, a.out,
+                          a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh);
   }
 }
 
@@ -740,13 +765,17 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
 // every other (kd, channel) chunk with its own halo buffers, and sums the two halves through LDS
 // before the epilogue -- split-K inside one workgroup, with no partial sums through memory and
 // no reduce pass; each group then runs the epilogue of half of the fragments.
-template <int KS, int BM, int TR, int WM, bool D3, int KG = 1>
+// STR = 2: stride-2 volume conv (fsmi_conv3d_s2_halo_x3): the staged window covers the strided
+// input footprint of the TR x 32 output tile and tap (dh, dw) of output (r, c) reads window pixel
+// (2r + dh, 2c + dw).
+template <int KS, int BM, int TR, int WM, bool D3, int KG = 1, int STR = 1>
 __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
   static_assert(KG == 1 || KG == 2, "K groups: 1 or 2");
-  using HS = HaloStage<KS, TR>;
+  static_assert(STR == 1 || (STR == 2 && D3 && KS == 3), "stride 2: 3x3x3 volumes only");
+  using HS = HaloStage<KS, TR, STR>;
   constexpr int RM = range_mode<D3>();
   __shared__ __attribute__((aligned(16))) _Float16 Xh[KG][HS::NHP][HROW];
   __shared__ __attribute__((aligned(16))) _Float16 Xl[KG][HS::NHP][HROW];
@@ -831,7 +860,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
           }
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+            const int hp = ((wn * TN + j) * STR + dh) * HS::HC + STR * rl + dw;
             bh[j] = *reinterpret_cast<const half8*>(&gXh[hp][16 * k + 8 * hsel]);
             bl[j] = *reinterpret_cast<const half8*>(&gXl[hp][16 * k + 8 * hsel]);
           }
@@ -870,7 +899,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
         }
         hs.template store<RM>(gXh, gXl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
         if (cc + KG < cc_end && !(a.dbg & 2)) {
-          if constexpr (D3) hs.load(a, tc.b, (cc + KG) % nck, tc.d0 + (cc + KG) / nck - a.PDD + a.sd);
+          if constexpr (D3) hs.load(a, tc.b, (cc + KG) % nck, STR * tc.d0 + (cc + KG) / nck - a.PDD + a.sd);
           else hs.load(a, tc.b, cc + KG);
         }   // in flight during this chunk's taps
       }
@@ -878,7 +907,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
     };
     if (n_g > 0) {
       load_wf(std::integral_constant<int, 0>(), c_first, 0);
-      if constexpr (D3) hs.load(a, tc.b, c_first % nck, tc.d0 + c_first / nck - a.PDD + a.sd);
+      if constexpr (D3) hs.load(a, tc.b, c_first % nck, STR * tc.d0 + c_first / nck - a.PDD + a.sd);
       else hs.load(a, tc.b, c_first);
     }
     // chunks in pairs so every register-buffer index is static (parity 0, then 1)
@@ -963,11 +992,11 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
 }
 
-template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1>
+template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1, int STR = 1>
 void launch_tile(const HaloArgs& a, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit * (a.up == 2 ? 8 : 1);
   if constexpr (WREG)
-    hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3, KG>), dim3(grid), dim3(256 * KG), 0, s, a);
+    hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3, KG, STR>), dim3(grid), dim3(256 * KG), 0, s, a);
   else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);
 }
 

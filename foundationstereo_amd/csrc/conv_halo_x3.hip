@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
 #pragma unroll
   for (int k = 1; k < 8; ++k)
     if (k < a.nsplit) { v.x += p[k].x; v.y += p[k].y; v.z += p[k].z; v.w += p[k].w; }
-  if ((a.act <= 2 || a.act == 6) && !a.res) {      // plain epilogue: vector store
+  if ((a.act <= 2 || a.act == 6) && !a.res && !a.fatt) {      // plain epilogue: vector store
     const float2 q = a.sb[co];
     const float gg = a.gamma ? a.gamma[co] : 1.f;
     float r[4] = {v.x * q.x + q.y, v.y * q.x + q.y, v.z * q.x + q.y, v.w * q.x + q.y};
@@ -106,11 +106,14 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   FSMI_CHECK_ARG(nseg >= 1 && nseg <= kHMaxSeg, "%s: 1..%d segments, got %d", what, kHMaxSeg, nseg);
   FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "%s: bad shape", what);
   FSMI_CHECK_ARG(KS == 1 || KS == 3 || (KS == 2 && a.up && KD == 2), "%s: kernel %d unsupported (1, 3)", what, KS);
+  if (a.str == 0) a.str = 1;
+  FSMI_CHECK_ARG(a.str == 1 || (a.str == 2 && KS == 3 && KD == 3 && !a.up), "%s: stride 2 needs a 3x3x3 kernel", what);
   FSMI_CHECK_ARG(D >= 1 && KD >= 1 && (KD % 2 == 1 || a.up), "%s: depth %d / depth kernel %d (odd)", what, D, KD);
   FSMI_CHECK_ARG(a.act == 3 || (out && co0 >= 0 && co0 + Cout <= out_ctot), "%s: output slice outside the tensor",
                  what);
   int cin = 0;
   const long long HW = static_cast<long long>(D) * H * W;     // channel stride
+  const long long IHW = a.str == 2 ? a.icstride : HW;          // the input's (stride 2: D, H, W are the output's)
   a.D = D;
   a.KD = KD;
   a.PDD = KD / 2;
@@ -120,7 +123,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     FSMI_CHECK_ARG(i == nseg - 1 || seg_ch[i] % 8 == 0,
                    "%s: inner segments must be multiples of 8 channels (segment %d: %d)", what, i, seg_ch[i]);
     a.seg_ptr[i] = seg_ptr[i];
-    a.seg_bstride[i] = static_cast<long long>(seg_ctot[i]) * HW;
+    a.seg_bstride[i] = static_cast<long long>(seg_ctot[i]) * IHW;
     cin += seg_ch[i];
     a.seg_end[i] = cin;
   }
@@ -164,7 +167,10 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     cfg -= 16;
     FSMI_CHECK_ARG(halo::kg2_tile(cfg), "%s: tile %d has no K-group variant (16 + 3/4/5/7)", what, cfg);
   }
-  FSMI_CHECK_ARG((cfg >= 0 && cfg <= 9) || pw, "%s: cfg %d (0..9, 16 + 3/4/5/7, 24..26)", what, cfg);
+  FSMI_CHECK_ARG((cfg >= 0 && cfg <= 9) || pw || (a.str == 2 && cfg == 10), "%s: cfg %d (0..9, 16 + 3/4/5/7, 24..26)",
+                 what, cfg);
+  FSMI_CHECK_ARG(a.str == 1 || (kg == 1 && (cfg == 4 || cfg == 5 || cfg == 7 || cfg == 10)),
+                 "%s: stride-2 tile %d (4, 5, 7, 10)", what, cfg);
   if (pw) halo::pw_tile(cfg, a);
   else switch (cfg) {                             // tile = couts x (rows x 32 px)
     case 0: case 2: tile_counts<3, 64, 8, 1>(a); break;
@@ -174,6 +180,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     case 6: tile_counts<3, 32, 8, 1>(a); break;
     case 8: tile_counts<3, 128, 8, 2>(a); break;
     case 9: tile_counts<3, 256, 4, 4>(a); break;
+    case 10: tile_counts<3, 64, 2, 2>(a); break;
     default: tile_counts<3, 32, 4, 1>(a); break;
   }
   const int nck = KD * a.CinP / HKC;               // split-K runs over (kd, channel chunk) pairs
@@ -212,7 +219,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     return e ? std::atoi(e) : 0;
   }();
   a.dbg = conv_dbg;
-  const int rc = pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
+  const int rc = a.str == 2 ? halo::launch_s2(cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
   if (a.nsplit > 1) halo::split_reduce(a, s);
@@ -267,15 +274,30 @@ extern "C" int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* 
                   out_ctot, co0, B, Cout, KS, H, W, cfg, nsplit, ws, ws_floats, stream);
 }
 
-extern "C" int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wlo, const float* scale_bias,
-                                   const float* res, float* out, int B, int Cout, int D, int H,
-                                   int W, int KD, int KS, int act, int res_pre, int cfg, int nsplit, float* ws,
-                                   long long ws_floats, void* stream) {
+extern "C" int fsmi_conv3d_halo_x3_ex(const float* x, int Cin, const void* whi, const void* wlo,
+                                      const float* scale_bias, const float* res, const float* fatt, float* out, int B,
+                                      int Cout, int D, int H, int W, int KD, int KS, int stride, int act, int res_pre,
+                                      int cfg, int nsplit, float* ws, long long ws_floats, void* stream) {
   FSMI_CHECK_ARG(x && out && Cin > 0, "fsmi_conv3d_halo_x3: null pointer / channels");
   FSMI_CHECK_ARG(act == 0 || act == 1 || act == 6, "fsmi_conv3d_halo_x3: act %d (0 none, 1 ReLU, 6 LeakyReLU)", act);
+  FSMI_CHECK_ARG(stride == 1 || stride == 2, "fsmi_conv3d_halo_x3: stride %d (1, 2)", stride);
+  FSMI_CHECK_ARG(B > 0 && D > 0 && H > 0 && W > 0, "fsmi_conv3d_halo_x3: bad shape");
   HaloArgs a{};
   a.act = act;
   a.alpha = 1.f;
+  a.fatt = fatt;
+  a.str = stride;
+  if (stride == 2) {                               // k3 s2 p1: output (n - 1) / 2 + 1 per dimension
+    FSMI_CHECK_ARG(KD == 3 && KS == 3 && !res, "fsmi_conv3d_halo_x3: stride 2 is a 3x3x3 conv without residual");
+    a.iD = D;
+    a.iH = H;
+    a.iW = W;
+    a.icstride = static_cast<long long>(D) * H * W;
+    D = (D - 1) / 2 + 1;
+    H = (H - 1) / 2 + 1;
+    W = (W - 1) / 2 + 1;
+    if (cfg < 0) cfg = Cout <= 64 ? 10 : 4;          // TR = 2 tiles: 52 KB of LDS, three blocks per CU
+  }
   a.res = res;
   a.res_pre = res_pre;
   a.res_bstride = static_cast<long long>(Cout) * D * H * W;
@@ -283,6 +305,14 @@ extern "C" int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, con
   const int ch[1] = {Cin}, tot[1] = {Cin};
   return run_halo(a, "fsmi_conv3d_halo_x3", seg, ch, tot, 1, whi, wlo, scale_bias, out, Cout, 0, B, Cout, KS, H, W,
                   cfg, nsplit, ws, ws_floats, stream, D, KD);
+}
+
+extern "C" int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wlo, const float* scale_bias,
+                                   const float* res, float* out, int B, int Cout, int D, int H,
+                                   int W, int KD, int KS, int act, int res_pre, int cfg, int nsplit, float* ws,
+                                   long long ws_floats, void* stream) {
+  return fsmi_conv3d_halo_x3_ex(x, Cin, whi, wlo, scale_bias, res, nullptr, out, B, Cout, D, H, W, KD, KS, 1, act,
+                                res_pre, cfg, nsplit, ws, ws_floats, stream);
 }
 
 extern "C" int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* const* whi, const void* const* wlo,

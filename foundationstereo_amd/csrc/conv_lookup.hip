@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void conv_lookup_kernel(HaloArgs a, LookupConv
       const long long p = px0 + j * 32 + rl;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        store_frag<ACT, false>(a, acc[i][j], xinv, (wm * TM + i) * 32 + 4 * hsel, b, p, a.out, a.sb, a.gamma, a.res,
+        store_frag<ACT, false>(a, acc[i][j], xinv, (wm * TM + i) * 32 + 4 * hsel, b, p, 0, a.out, a.sb, a.gamma, a.res,
                                a.gh, a.gz, a.gatt, a.grh);
     }
   };

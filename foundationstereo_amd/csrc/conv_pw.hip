@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
       const long long hw = px0 + (wn * TN + j) * 32 + rl;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        store_frag<ACT, false>(a, acc[i][j], xinv, m0 + (wm * TM + i) * 32 + 4 * hsel, b, hw, a.out, a.sb, a.gamma,
+        store_frag<ACT, false>(a, acc[i][j], xinv, m0 + (wm * TM + i) * 32 + 4 * hsel, b, hw, 0, a.out, a.sb, a.gamma,
                                a.res, a.gh, a.gz, a.gatt, a.grh);
     }
   };

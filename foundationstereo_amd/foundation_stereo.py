@@ -9,7 +9,8 @@ is the data path:
   the 32-channel comb volume and its cat copy never exist in HBM;
 * a3: 3D filtering: every stride-1 Conv3d + BN block on the halo split-precision kernel
   (``ops.conv3d``), the classifier head on ``ops.conv3d_direct``, the disparity transformer
-  on ``ops.disparity_transformer``; strided / transposed 3D convs on MIOpen;
+  on ``ops.disparity_transformer``, the stride-2 convs and ConvTranspose3d on the halo
+  kernel's stride-2 / phase tiles, FeatureAtt folded into the producing conv's epilogue;
 * a4: softmax + soft-argmin fused (``ops.softmax_regression``); skipped when an
   ``init_disp`` is supplied (hierarchical pass) since the reference discards it;
 * a5/a6: geometry encoding + per-iteration lookup on HIP (``geometry.py``);
@@ -53,6 +54,14 @@ def normalize_image(img):
 
 
 _NORM_CACHE = {}
+
+
+def _gated(seq, x, gate):
+    """seq(x) * sigmoid(gate) broadcast over depth, the gate applied by seq's last block
+    (a Conv3dNormActReduced: its second conv's epilogue)."""
+    for m in list(seq)[:-1]:
+        x = m(x)
+    return seq[-1](x, fatt=gate)
 
 
 class hourglass(nn.Module):
@@ -100,11 +109,20 @@ class hourglass(nn.Module):
         self.feature_att_up_8 = FeatureAtt(2 * c, feat_dims[1])
 
     def forward(self, x, features):
-        c1 = self.feature_att_8(self.conv1(x), features[1])
-        c2 = self.feature_att_16(self.conv2(c1), features[2])
-        c3 = self.feature_att_32(self.conv3(c2), features[3])
-        c2 = self.feature_att_up_16(self.agg_0(torch.cat((self.conv3_up(c3), c2), dim=1)), features[2])
-        c1 = self.feature_att_up_8(self.agg_1(torch.cat((self.conv2_up(c2), c1), dim=1)), features[1])
+        if _sub.FATT_FUSE and not self.training:
+            # each FeatureAtt's sigmoid(gate) * cv in the epilogue of the conv that produces cv
+            # (core/foundation_stereo.py:93-109, core/submodule.py:452-453)
+            c1 = _gated(self.conv1, x, self.feature_att_8.logits(features[1]))
+            c2 = _gated(self.conv2, c1, self.feature_att_16.logits(features[2]))
+            c3 = _gated(self.conv3, c2, self.feature_att_32.logits(features[3]))
+            c2 = _gated(self.agg_0, torch.cat((self.conv3_up(c3), c2), dim=1), self.feature_att_up_16.logits(features[2]))
+            c1 = _gated(self.agg_1, torch.cat((self.conv2_up(c2), c1), dim=1), self.feature_att_up_8.logits(features[1]))
+        else:
+            c1 = self.feature_att_8(self.conv1(x), features[1])
+            c2 = self.feature_att_16(self.conv2(c1), features[2])
+            c3 = self.feature_att_32(self.conv3(c2), features[3])
+            c2 = self.feature_att_up_16(self.agg_0(torch.cat((self.conv3_up(c3), c2), dim=1)), features[2])
+            c1 = self.feature_att_up_8(self.agg_1(torch.cat((self.conv2_up(c2), c1), dim=1)), features[1])
         conv = self.conv1_up(c1)
         if self._dt_fast(x, conv):
             # patch embed, transformer and the x4 trilinear add on HIP (csrc/transformer.hip)

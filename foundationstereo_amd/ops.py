@@ -367,28 +367,38 @@ _ACT3D = {None: 0, "relu": 1, "leaky": 6}
 
 
 def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res_pre: bool = False,
-           cfg: int = -1, nsplit: int = -1) -> Tensor:
-    """Stride-1 'same' Conv3d (KD x K x K, K in {1, 3}, KD odd) on the halo split-precision
-    kernel (``fsmi_conv3d_halo_x3``); NCDHW in and out.  ``act`` None / "relu" / "leaky" (0.01);
-    ``res`` is added after the activation, or before it with ``res_pre`` (ResNet block tail)."""
+           cfg: int = -1, nsplit: int = -1, stride: int = 1, fatt: Tensor = None) -> Tensor:
+    """'Same' Conv3d (KD x K x K, K in {1, 3}, KD odd) on the halo split-precision kernel
+    (``fsmi_conv3d_halo_x3_ex``); NCDHW in and out.  ``act`` None / "relu" / "leaky" (0.01);
+    ``res`` is added after the activation, or before it with ``res_pre`` (ResNet block tail).
+    ``stride`` 2: a 3x3x3 conv with padding 1 and stride 2 (output (n - 1) // 2 + 1 per dimension).
+    ``fatt``: FeatureAtt's pre-sigmoid gate (B, Cout, Ho, Wo); the output is multiplied by
+    sigmoid(fatt) broadcast over depth (core/submodule.py:452-453)."""
     assert pk.mode == "halo" and x.dim() == 5
-    _check("conv3d", x, *[t for t in (bias, res) if t is not None])
+    assert stride in (1, 2) and (stride == 1 or (pk.k == 3 and pk.kd == 3 and res is None)), \
+        "conv3d: stride 2 is a 3x3x3 conv without residual"
+    _check("conv3d", x, *[t for t in (bias, res, fatt) if t is not None])
     B, Cin, D, H, W = x.shape
     assert Cin == pk.cin, f"conv3d: {Cin} input channels for a conv packed with {pk.cin}"
     x = _c(x)
-    out = torch.empty((B, pk.cout, D, H, W), device=x.device, dtype=torch.float32)
+    Do, Ho, Wo = (D, H, W) if stride == 1 else ((D - 1) // 2 + 1, (H - 1) // 2 + 1, (W - 1) // 2 + 1)
+    out = torch.empty((B, pk.cout, Do, Ho, Wo), device=x.device, dtype=torch.float32)
     if res is not None:
         res = _c(res)
         assert res.shape == out.shape
+    if fatt is not None:
+        fatt = _c(fatt)
+        assert tuple(fatt.shape) == (B, pk.cout, Ho, Wo), f"conv3d: gate {tuple(fatt.shape)} for output {tuple(out.shape)}"
     if _CONV_FLOPS["on"]:
-        _CONV_FLOPS["flops"] += 2 * Cin * pk.cout * pk.kd * pk.k * pk.k * B * D * H * W
+        _CONV_FLOPS["flops"] += 2 * Cin * pk.cout * pk.kd * pk.k * pk.k * B * Do * Ho * Wo
     stream = _stream(x)
-    ws = _split_workspace(x.device, stream, 8 * B * pk.cout * D * H * W)
-    cfg, nsplit = _tuned(pk.k, pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
-    _lib.check(_lib.load().fsmi_conv3d_halo_x3(
+    ws = _split_workspace(x.device, stream, 8 * B * pk.cout * Do * Ho * Wo)
+    cfg, nsplit = _tuned(pk.k if stride == 1 else f"{pk.k}s2", pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
+    _lib.check(_lib.load().fsmi_conv3d_halo_x3_ex(
         _p(x), Cin, _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
-        _p(res) if res is not None else None, _p(out), B, pk.cout, D, H, W, pk.kd, pk.k, _ACT3D[act],
-        1 if res_pre else 0, cfg, nsplit, _p(ws), ws.numel(), stream), "conv3d")
+        _p(res) if res is not None else None, _p(fatt) if fatt is not None else None, _p(out), B, pk.cout,
+        D, H, W, pk.kd, pk.k, stride, _ACT3D[act], 1 if res_pre else 0, cfg, nsplit, _p(ws), ws.numel(), stream),
+        "conv3d")
     return out
 
 

@@ -7,7 +7,9 @@ so ``core.foundation_stereo`` can star-import this module instead
 Stride-1 3D conv blocks (``BasicConv``, ``Conv3dNormActReduced``,
 ``ResnetBasicBlock3D``) and stride-1 2D ``BasicConv``s run the halo split-precision
 conv kernel with the eval BatchNorm folded into the packed weights (``conv3d_bn_act``,
-``conv2d_bn_act``); strided / transposed convs stay on MIOpen through ``torch.nn``.
+``conv2d_bn_act``), the 3x3x3 stride-2 convs on its stride-2 tiles and the ConvTranspose3d
+(k4, s2) on its 2x2x2 phase tiles; other strided convs (2D) stay on MIOpen through ``torch.nn``.
+``FeatureAtt.logits`` gives the gate that the hourglass folds into its producing conv.
 Under autocast the HIP paths still run (inputs cast up, fp32 compute).
 
 The disparity transformer runs as one HIP kernel (``ops.disparity_transformer``); its
@@ -57,7 +59,11 @@ FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
 # sent there (A/B knob).
 UP3D = os.environ.get("FSMI_UP3D", "1") != "0"
 UP3D_MINVOX = int(os.environ.get("FSMI_UP3D_MINVOX", "0"))
-DT_FAST = os.environ.get("FSMI_DT", "1") != "0"      # disparity transformer on csrc/transformer.hip
+DT_FAST = os.environ.get("FSMI_DT", "1") != "0"
+# stride-2 3x3x3 convs on the halo kernel's stride-2 tiles (FSMI_S2=0: MIOpen, for A/B)
+S2_3D = os.environ.get("FSMI_S2", "1") != "0"
+# FeatureAtt's sigmoid(gate) * cv folded into the producing conv's epilogue (FSMI_FATT=0: ATen)
+FATT_FUSE = os.environ.get("FSMI_FATT", "1") != "0"      # disparity transformer on csrc/transformer.hip
 
 
 # Input dtypes the HIP paths accept.  Under the reference's fp16 autocast (scripts/run_demo.py:161)
@@ -79,6 +85,19 @@ def _fast3d(x, conv, bn) -> bool:
     kd, kh, kw = conv.kernel_size
     if conv.stride != (1, 1, 1) or conv.dilation != (1, 1, 1) or conv.groups != 1 or kh != kw or kh not in (1, 3) \
             or kd % 2 == 0 or conv.padding != (kd // 2, kh // 2, kw // 2):
+        return False
+    return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm3d and not bn.training
+                                                         and bn.track_running_stats)
+
+
+def _fast_s2_3d(x, conv, bn) -> bool:
+    """Conv3d(k=3, s=2, p=1) (+ eval BatchNorm3d): the hourglass downsampling convs
+    (core/foundation_stereo.py:50-58) on the halo kernel's stride-2 tiles."""
+    if not (FILTER3D and S2_3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+            and type(conv) is nn.Conv3d):
+        return False
+    if conv.kernel_size != (3, 3, 3) or conv.stride != (2, 2, 2) or conv.padding != (1, 1, 1) \
+            or conv.dilation != (1, 1, 1) or conv.groups != 1:
         return False
     return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm3d and not bn.training
                                                          and bn.track_running_stats)
@@ -163,10 +182,12 @@ def conv2d_bn_act(segs, conv, bn, act=None, **kw):
     return ops.conv2d(segs, pk, bias=b, act=act, **kw)
 
 
-def conv3d_bn_act(x, conv, bn, act=None, res=None, res_pre=False):
-    """act(bn(conv(x)) [+ res]) on the halo kernel (see ``_fast3d`` for when it applies)."""
+def conv3d_bn_act(x, conv, bn, act=None, res=None, res_pre=False, fatt=None):
+    """act(bn(conv(x)) [+ res]) [* sigmoid(fatt)] on the halo kernel (``_fast3d`` / ``_fast_s2_3d``
+    say when it applies; the conv's stride is taken from the module)."""
     pk, b = _packed_bn(conv, bn)
-    return ops.conv3d(_f32(x), pk, bias=b, act=act, res=None if res is None else _f32(res), res_pre=res_pre)
+    return ops.conv3d(_f32(x), pk, bias=b, act=act, res=None if res is None else _f32(res), res_pre=res_pre,
+                      stride=conv.stride[0], fatt=None if fatt is None else _f32(fatt))
 
 
 def _norm(kind, ch, is_3d):
@@ -192,7 +213,7 @@ class BasicConv(nn.Module):
 
     def forward(self, x):
         bn = self.bn if self.use_bn else None
-        if _fast3d(x, self.conv, bn):        # stride-1 3D conv + folded BN + LeakyReLU, one kernel
+        if _fast3d(x, self.conv, bn) or _fast_s2_3d(x, self.conv, bn):   # 3D conv + folded BN + LeakyReLU
             return conv3d_bn_act(x, self.conv, bn, "leaky" if self.relu else None)
         if UP3D and _fast_up3d(x, self.conv, bn):   # ConvTranspose3d k4 s2: 8 phase convs, BN folded
             packs, b = _packed_up(self.conv, bn)
@@ -218,13 +239,16 @@ class Conv3dNormActReduced(nn.Module):
             nn.Conv3d(hidden, C_out, kernel_size=(kd, 1, 1), padding=(kd // 2, 0, 0), stride=(stride, 1, 1)),
             norm(C_out), nn.ReLU())
 
-    def forward(self, x):
+    def forward(self, x, fatt=None):
+        """``fatt``: a following FeatureAtt's pre-sigmoid gate (``FeatureAtt.logits``), applied in the
+        second conv's epilogue (returns sigmoid(fatt).unsqueeze(2) * block(x))."""
         c1, c2 = self.conv1, self.conv2
         if _fast3d(x, c1[0], c1[1]) and _fast3d(x, c2[0], c2[1]) and isinstance(c1[2], nn.ReLU) \
                 and isinstance(c2[2], nn.ReLU):
             y = conv3d_bn_act(x, c1[0], c1[1], "relu")
-            return conv3d_bn_act(y, c2[0], c2[1], "relu")
-        return self.conv2(self.conv1(x))
+            return conv3d_bn_act(y, c2[0], c2[1], "relu", fatt=fatt)
+        y = self.conv2(self.conv1(x))
+        return y if fatt is None else torch.sigmoid(fatt).unsqueeze(2) * y
 
 
 class _ResBlock(nn.Module):
@@ -481,8 +505,17 @@ class FeatureAtt(nn.Module):
         self.feat_att = nn.Sequential(BasicConv(feat_chan, feat_chan // 2, kernel_size=1, stride=1, padding=0),
                                       nn.Conv2d(feat_chan // 2, cv_chan, 1))
 
+    def logits(self, feat):
+        """feat_att(feat): the pre-sigmoid gate (B, cv_chan, H, W); both 1x1 convs on the halo kernel
+        when they qualify (the hourglass folds sigmoid(gate) * cv into the producing conv)."""
+        c0, c1 = self.feat_att
+        h = c0(feat)
+        if _fast2d(h, c1, None):
+            return conv2d_bn_act([h], c1, None)
+        return c1(h)
+
     def forward(self, cv, feat):
-        return torch.sigmoid(self.feat_att(feat)).unsqueeze(2) * cv
+        return torch.sigmoid(self.logits(feat)).unsqueeze(2) * cv
 
 
 class PositionalEmbedding(nn.Module):

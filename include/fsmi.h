@@ -242,6 +242,20 @@ int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wl
                         const float* res, float* out, int B, int Cout, int D, int H, int W, int KD, int KS,
                         int act, int res_pre, int cfg, int nsplit, float* ws, long long ws_floats, void* stream);
 
+/* ---- a3: stride-2 Conv3d and the fused FeatureAtt gate ----------------------
+ * fsmi_conv3d_halo_x3 with two more terms:
+ *   stride 2: the hourglass BasicConv(is_3d, kernel_size=3, stride=2, padding=1) + BN + LeakyReLU
+ *     (core/foundation_stereo.py:50-58): D, H, W are the INPUT's, out is
+ *     (B, Cout, (D-1)/2+1, (H-1)/2+1, (W-1)/2+1); KD = KS = 3, no residual; cfg -1 or the
+ *     stride-2 tiles 4 (128 couts x 2x32 px), 5 (64 x 4x32), 7 (32 x 4x32), 10 (64 x 2x32).
+ *   fatt: FeatureAtt (core/submodule.py:438-454) folded into the epilogue -- the final value of
+ *     output channel co at (d, h, w) is multiplied by sigmoid(fatt[b, co, h, w]); fatt is the
+ *     gate's pre-sigmoid (B, Cout, Ho, Wo) map (contiguous) or NULL. */
+int fsmi_conv3d_halo_x3_ex(const float* x, int Cin, const void* whi, const void* wlo, const float* scale_bias,
+                           const float* res, const float* fatt, float* out, int B, int Cout, int D, int H, int W,
+                           int KD, int KS, int stride, int act, int res_pre, int cfg, int nsplit, float* ws,
+                           long long ws_floats, void* stream);
+
 /* ---- refinement-loop auxiliaries ---------------------------------------
  * fsmi_dwconv2d: depthwise KSxKS conv (KS in {3,5,7}, stride 1, zero pad KS/2)
  *   x, out (B,C,H,W); w (C,1,KS,KS); bias (C) or NULL.  Replaces the EdgeNeXt

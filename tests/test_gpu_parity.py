@@ -251,6 +251,74 @@ def test_conv3d_up2_vs_torch(ops_mod, cin, cout, D, H, W, B, cfg):
     close(out, ref, atol=2e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("cfg,nsplit", [(-1, -1), (4, 1), (5, 1), (7, 1), (10, 1), (10, 3), (4, 2)])
+@pytest.mark.parametrize("cin,cout,D,H,W,B", [(28, 56, 12, 19, 70, 1), (56, 112, 7, 10, 40, 2),
+                                              (112, 168, 6, 15, 20, 1), (40, 37, 5, 9, 65, 1)])
+def test_conv3d_s2_vs_torch(ops_mod, cin, cout, D, H, W, B, cfg, nsplit):
+    """Conv3d(k=3, s=2, p=1) + folded BN + LeakyReLU (the hourglass conv1/2/3 downsampling,
+    core/foundation_stereo.py:50-58) on the stride-2 halo tiles vs fp64 torch: even and odd input
+    sizes (output (n-1)//2+1), ragged row / column / cout tiles and channel chunks, batch 2,
+    split-K, every stride-2 tile; 2e-5 abs + 1e-5 rel as the stride-1 volume convs."""
+    import torch.nn.functional as F
+    gen = torch.Generator().manual_seed(cin + cout + D + H)
+    x = torch.randn(B, cin, D, H, W, generator=gen)
+    w = torch.randn(cout, cin, 3, 3, 3, generator=gen) * 0.05
+    bias = torch.randn(cout, generator=gen) * 0.1
+    out = ops_mod.conv3d(g(x), ops_mod.PackedConv(g(w), mode="halo"), bias=g(bias), act="leaky", stride=2,
+                         cfg=cfg, nsplit=nsplit)
+    ref = F.leaky_relu(F.conv3d(x.double(), w.double(), bias.double(), stride=2, padding=1), 0.01)
+    assert out.shape == ref.shape
+    close(out, ref, atol=2e-5, rtol=1e-5)
+    assert not ops_mod.range_overflowed(reset=True)
+
+
+@pytest.mark.parametrize("nsplit", [1, 2])
+@pytest.mark.parametrize("kern,stride,cfg", [((17, 1, 1), 1, -1), ((17, 1, 1), 1, 7), ((3, 3, 3), 2, 10),
+                                             ((1, 3, 3), 1, 5)])
+def test_conv3d_feature_gate_vs_torch(ops_mod, kern, stride, cfg, nsplit):
+    """FeatureAtt (core/submodule.py:438-454) folded into the producing conv's epilogue:
+    relu(conv(x) + b) * sigmoid(gate) broadcast over depth, gate (B, Cout, Ho, Wo), with and
+    without split-K (the reduce pass applies it), vs fp64 torch."""
+    import torch.nn.functional as F
+    gen = torch.Generator().manual_seed(7 + kern[0] + stride)
+    B, cin, cout, D, H, W = 2, 56, 56, 12, 9, 37
+    x = torch.randn(B, cin, D, H, W, generator=gen)
+    w = torch.randn(cout, cin, *kern, generator=gen) * 0.05
+    bias = torch.randn(cout, generator=gen) * 0.1
+    pad = tuple(k // 2 for k in kern)
+    y = F.conv3d(x.double(), w.double(), bias.double(), stride=stride, padding=pad)
+    gate = torch.randn(B, cout, y.shape[3], y.shape[4], generator=gen) * 3
+    ref = F.relu(y) * torch.sigmoid(gate.double()).unsqueeze(2)
+    out = ops_mod.conv3d(g(x), ops_mod.PackedConv(g(w), mode="halo"), bias=g(bias), act="relu", stride=stride,
+                         fatt=g(gate), cfg=cfg, nsplit=nsplit)
+    close(out, ref, atol=2e-5, rtol=1e-5)
+
+
+def test_hourglass_gated_vs_unfused(ops_mod):
+    """hourglass with every FeatureAtt folded into its producing conv and the stride-2 convs on
+    HIP vs the same module with both off (FeatureAtt as sigmoid * cv in ATen, stride-2 on
+    MIOpen), fp32 on the same weights."""
+    from foundationstereo_amd import submodule as sub
+    from foundationstereo_amd.foundation_stereo import hourglass
+    C, fd = 8, [48, 64, 192, 160]
+    m = hourglass({"max_disp": 64}, C, fd).eval()
+    synth.init_module_(m, seed=77)
+    m = m.to(DEV)
+    B, D, H, W = 1, 16, 24, 32
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(B, C, D, H, W, generator=gen).to(DEV)
+    feats = [torch.randn(B, fd[i], H // 2 ** i, W // 2 ** i, generator=gen).to(DEV) for i in range(4)]
+    with torch.no_grad():
+        a = m(x, feats)
+        old = sub.FATT_FUSE, sub.S2_3D
+        try:
+            sub.FATT_FUSE, sub.S2_3D = False, False
+            b = m(x, feats)
+        finally:
+            sub.FATT_FUSE, sub.S2_3D = old
+    close(a, b.double(), atol=5e-5, rtol=5e-5)
+
+
 @pytest.mark.parametrize("L,Cv,D,H,W,B,nsplit", [(4, 28, 48, 12, 40, 1, 1), (2, 8, 24, 5, 37, 2, 2),
                                                    (4, 28, 48, 30, 40, 1, 3), (3, 28, 80, 7, 64, 1, 2)])
 def test_conv1x1_lookup_vs_unfused(ops_mod, L, Cv, D, H, W, B, nsplit):

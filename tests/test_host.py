@@ -112,6 +112,11 @@ def test_conv_tuning_db_wellformed():
         db = json.load(f)
     assert db["entries"], "empty tuning table"
     for key, e in db["entries"].items():
+        if key.startswith("k3s2_"):        # stride-2 3x3x3 volume convs: their own tiles 4 / 5 / 7 / 10
+            ks, stride, kd, cin, cout, B, D, H, W = (int(v) for v in re.findall(r"\d+", key))
+            assert key == ops._tune_key(f"{ks}s{stride}", kd, cin, cout, B, D, H, W) and kd == 3
+            assert e["cfg"] in (4, 5, 7, 10) and 1 <= e["nsplit"] <= 8, (key, e)
+            continue
         ks, kd, cin, cout, B, D, H, W = (int(v) for v in re.findall(r"\d+", key))
         assert key == ops._tune_key(ks, kd, cin, cout, B, D, H, W)
         assert ks in (1, 3) and kd % 2 == 1 and min(cin, cout, B, D, H, W) > 0
