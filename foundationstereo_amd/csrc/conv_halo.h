@@ -126,8 +126,8 @@ int launch_cfg(int cfg, int kg, const HaloArgs& a, hipStream_t s);
 // Pointwise tiles (cfg 24-26, conv_pw.hip): 1x1 2D layers with an LDS-DMA input ring.
 // pw_tile sets the tile geometry (a.nct = pixel tiles per image, npix, nco) before split-K.
 int launch_pw(int cfg, const HaloArgs& a, hipStream_t s);
-// stride-2 3x3x3 volume tiles (conv_halo_s2_3d.hip, fsmi_conv3d_s2_halo_x3)
-int launch_s2(int cfg, const HaloArgs& a, hipStream_t s);
+// stride-2 tiles, KS x KS (KS in {1, 3}) planes of the volume kernel (conv_halo_s2_3d.hip)
+int launch_s2(int ks, int cfg, const HaloArgs& a, hipStream_t s);
 // split-K reduce pass over a.ws (conv_halo_x3.hip)
 void split_reduce(const HaloArgs& a, hipStream_t s);
 void pw_tile(int cfg, HaloArgs& a);
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
   static_assert(KG == 1 || KG == 2, "K groups: 1 or 2");
-  static_assert(STR == 1 || (STR == 2 && D3 && KS == 3), "stride 2: 3x3x3 volumes only");
+  static_assert(STR == 1 || (STR == 2 && D3 && (KS == 3 || KS == 1)), "stride 2: 3x3 / 1x1 tiles of the volume kernel");
   using HS = HaloStage<KS, TR, STR>;
   constexpr int RM = range_mode<D3>();
   __shared__ __attribute__((aligned(16))) _Float16 Xh[KG][HS::NHP][HROW];

@@ -107,7 +107,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "%s: bad shape", what);
   FSMI_CHECK_ARG(KS == 1 || KS == 3 || (KS == 2 && a.up && KD == 2), "%s: kernel %d unsupported (1, 3)", what, KS);
   if (a.str == 0) a.str = 1;
-  FSMI_CHECK_ARG(a.str == 1 || (a.str == 2 && KS == 3 && KD == 3 && !a.up), "%s: stride 2 needs a 3x3x3 kernel", what);
+  FSMI_CHECK_ARG(a.str == 1 || (a.str == 2 && (KS == 3 || KS == 1) && (KD == 3 || KD == 1) && !a.up),
+                 "%s: stride 2 needs a KD x KS x KS kernel with KS, KD in {1, 3}", what);
   FSMI_CHECK_ARG(D >= 1 && KD >= 1 && (KD % 2 == 1 || a.up), "%s: depth %d / depth kernel %d (odd)", what, D, KD);
   FSMI_CHECK_ARG(a.act == 3 || (out && co0 >= 0 && co0 + Cout <= out_ctot), "%s: output slice outside the tensor",
                  what);
@@ -219,7 +220,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     return e ? std::atoi(e) : 0;
   }();
   a.dbg = conv_dbg;
-  const int rc = a.str == 2 ? halo::launch_s2(cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
+  const int rc = a.str == 2 ? halo::launch_s2(KS, cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
   if (a.nsplit > 1) halo::split_reduce(a, s);
@@ -287,8 +288,11 @@ extern "C" int fsmi_conv3d_halo_x3_ex(const float* x, int Cin, const void* whi, 
   a.alpha = 1.f;
   a.fatt = fatt;
   a.str = stride;
-  if (stride == 2) {                               // k3 s2 p1: output (n - 1) / 2 + 1 per dimension
-    FSMI_CHECK_ARG(KD == 3 && KS == 3 && !res, "fsmi_conv3d_halo_x3: stride 2 is a 3x3x3 conv without residual");
+  // the 2D instantiation (D = KD = 1 at stride 1) has no res_pre path
+  FSMI_CHECK_ARG(!res_pre || D > 1 || KD > 1 || stride == 2, "fsmi_conv3d_halo_x3: res_pre needs a volume (D or KD > 1)"
+                 " or stride 2");
+  if (stride == 2) {                               // k3 p1 / k1 p0, stride 2: output (n - 1) / 2 + 1 per dimension
+    FSMI_CHECK_ARG((KS == 3 || KS == 1) && (KD == 3 || KD == 1), "fsmi_conv3d_halo_x3: stride 2 needs KS, KD in {1, 3}");
     a.iD = D;
     a.iH = H;
     a.iW = W;

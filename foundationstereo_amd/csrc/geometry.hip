@@ -249,7 +249,10 @@ __global__ __launch_bounds__(256) void volume_pyramid_kernel(const float* __rest
 // once per channel into registers; each tap selects its pair with
 // compile-time indices (no scratch), so a channel costs 2r+4 loads, not 4r+2.
 // ---------------------------------------------------------------------------
-constexpr int kCPC = 4;  // geo channels per wave
+#ifndef FSMI_LOOKUP_CPC
+#define FSMI_LOOKUP_CPC 4
+#endif
+constexpr int kCPC = FSMI_LOOKUP_CPC;  // geo channels per wave
 
 struct LookupArgs {
   const float* vol[FSMI_MAX_LEVELS];

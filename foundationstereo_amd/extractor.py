@@ -14,7 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import synth
-from .submodule import BasicConv, _fast2d, conv2d_bn_act
+from .submodule import BasicConv, _fast2d, _fast_s2_2d, conv2d_bn_act, conv2d_s2_bn_act
 
 __all__ = ["ResidualBlock", "ContextNetDino", "DepthAnythingFeature", "SyntheticFeature"]
 
@@ -58,12 +58,20 @@ class ResidualBlock(nn.Module):
         n1 = self.norm1 if isinstance(self.norm1, nn.BatchNorm2d) else None
         n2 = self.norm2 if isinstance(self.norm2, nn.BatchNorm2d) else None
         if n1 is not None and n2 is not None and _fast2d(x, self.conv2, n2):
-            # stride-1 convs on the halo kernel with the eval BN folded in; the strided first conv
-            # of a downsampling block and its 1x1 projection stay on MIOpen
-            y = conv2d_bn_act([x], self.conv1, n1, "relu") if _fast2d(x, self.conv1, n1) \
-                else F.relu(n1(self.conv1(x)))
+            # every conv on the halo kernel with the eval BN folded in: stride-1 convs as 2D maps,
+            # a downsampling block's 3x3 s2 conv and 1x1 s2 projection on the stride-2 tiles, the
+            # projection finishing the block: relu(bn3(proj(x)) + y) in its epilogue
+            if _fast2d(x, self.conv1, n1):
+                y = conv2d_bn_act([x], self.conv1, n1, "relu")
+            elif _fast_s2_2d(x, self.conv1, n1):
+                y = conv2d_s2_bn_act(x, self.conv1, n1, "relu")
+            else:
+                y = F.relu(n1(self.conv1(x)))
             y = conv2d_bn_act([y], self.conv2, n2, "relu")
             if self.downsample is not None:
+                pc, n3 = self.downsample
+                if isinstance(n3, nn.BatchNorm2d) and _fast_s2_2d(x, pc, n3):
+                    return conv2d_s2_bn_act(x, pc, n3, "relu", res=y, res_pre=True)
                 x = self.downsample(x)
             return torch.relu_(y.add_(x))
         y = F.relu(self.norm1(self.conv1(x)))

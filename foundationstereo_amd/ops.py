@@ -371,12 +371,13 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
     """'Same' Conv3d (KD x K x K, K in {1, 3}, KD odd) on the halo split-precision kernel
     (``fsmi_conv3d_halo_x3_ex``); NCDHW in and out.  ``act`` None / "relu" / "leaky" (0.01);
     ``res`` is added after the activation, or before it with ``res_pre`` (ResNet block tail).
-    ``stride`` 2: a 3x3x3 conv with padding 1 and stride 2 (output (n - 1) // 2 + 1 per dimension).
+    ``stride`` 2: KD x K x K with K, KD in {1, 3}, padding K // 2, KD // 2 and stride 2 (output
+    (n - 1) // 2 + 1 per dimension; 2D convs as volumes of depth 1).
     ``fatt``: FeatureAtt's pre-sigmoid gate (B, Cout, Ho, Wo); the output is multiplied by
     sigmoid(fatt) broadcast over depth (core/submodule.py:452-453)."""
     assert pk.mode == "halo" and x.dim() == 5
-    assert stride in (1, 2) and (stride == 1 or (pk.k == 3 and pk.kd == 3 and res is None)), \
-        "conv3d: stride 2 is a 3x3x3 conv without residual"
+    assert stride in (1, 2) and (stride == 1 or (pk.k in (1, 3) and pk.kd in (1, 3))), \
+        "conv3d: stride 2 needs K, KD in {1, 3}"
     _check("conv3d", x, *[t for t in (bias, res, fatt) if t is not None])
     B, Cin, D, H, W = x.shape
     assert Cin == pk.cin, f"conv3d: {Cin} input channels for a conv packed with {pk.cin}"

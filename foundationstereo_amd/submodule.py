@@ -103,6 +103,28 @@ def _fast_s2_3d(x, conv, bn) -> bool:
                                                          and bn.track_running_stats)
 
 
+def _fast_s2_2d(x, conv, bn) -> bool:
+    """Conv2d(k=3, s=2, p=1) or Conv2d(k=1, s=2, p=0) (+ eval BatchNorm2d): the context net's
+    downsampling convs, as depth-1 volumes on the halo kernel's stride-2 tiles."""
+    if not (FILTER3D and S2_3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+            and type(conv) is nn.Conv2d):
+        return False
+    k = conv.kernel_size
+    if k not in ((3, 3), (1, 1)) or conv.stride != (2, 2) or conv.padding != (k[0] // 2, k[1] // 2) \
+            or conv.dilation != (1, 1) or conv.groups != 1:
+        return False
+    return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm2d and not bn.training
+                                                         and bn.track_running_stats)
+
+
+def conv2d_s2_bn_act(x, conv, bn, act=None, res=None, res_pre=False):
+    """act(bn(conv(x)) [+ res]) for a stride-2 Conv2d (``_fast_s2_2d``): the volume kernel on
+    (B, C, 1, H, W)."""
+    pk, b = _packed_bn(conv, bn)
+    r = None if res is None else _f32(res).unsqueeze(2)
+    return ops.conv3d(_f32(x).unsqueeze(2), pk, bias=b, act=act, res=r, res_pre=res_pre, stride=2).squeeze(2)
+
+
 def _fast_up3d(x, conv, bn) -> bool:
     """ConvTranspose3d(k=4, s=2, p=1) (+ eval BatchNorm3d) that the 2x2x2 phase tiles run."""
     if not (FILTER3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()

@@ -245,9 +245,11 @@ int fsmi_conv3d_halo_x3(const float* x, int Cin, const void* whi, const void* wl
 /* ---- a3: stride-2 Conv3d and the fused FeatureAtt gate ----------------------
  * fsmi_conv3d_halo_x3 with two more terms:
  *   stride 2: the hourglass BasicConv(is_3d, kernel_size=3, stride=2, padding=1) + BN + LeakyReLU
- *     (core/foundation_stereo.py:50-58): D, H, W are the INPUT's, out is
- *     (B, Cout, (D-1)/2+1, (H-1)/2+1, (W-1)/2+1); KD = KS = 3, no residual; cfg -1 or the
- *     stride-2 tiles 4 (128 couts x 2x32 px), 5 (64 x 4x32), 7 (32 x 4x32), 10 (64 x 2x32).
+ *     (core/foundation_stereo.py:50-58), and with D = KD = 1 the context net's 3x3 s2 p1 convs and
+ *     1x1 s2 projections (core/extractor.py:20-80): KS, KD in {1, 3} with padding KS/2, KD/2;
+ *     D, H, W are the INPUT's, out / res are (B, Cout, (D-1)/2+1, (H-1)/2+1, (W-1)/2+1); cfg -1 or
+ *     the stride-2 tiles 4 (128 couts x 2x32 px), 5 (64 x 4x32), 7 (32 x 4x32), 10 (64 x 2x32).
+ *   res_pre needs a volume (D or KD > 1) or stride 2 (FSMI_ERR_ARG otherwise).
  *   fatt: FeatureAtt (core/submodule.py:438-454) folded into the epilogue -- the final value of
  *     output channel co at (d, h, w) is multiplied by sigmoid(fatt[b, co, h, w]); fatt is the
  *     gate's pre-sigmoid (B, Cout, Ho, Wo) map (contiguous) or NULL. */

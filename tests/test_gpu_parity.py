@@ -272,6 +272,40 @@ def test_conv3d_s2_vs_torch(ops_mod, cin, cout, D, H, W, B, cfg, nsplit):
     assert not ops_mod.range_overflowed(reset=True)
 
 
+@pytest.mark.parametrize("k,cin,cout,H,W,res", [(3, 64, 96, 120, 160, False), (1, 64, 96, 120, 160, True),
+                                                 (3, 96, 128, 31, 45, False), (1, 128, 128, 15, 20, True)])
+def test_conv2d_s2_vs_torch(ops_mod, k, cin, cout, H, W, res):
+    """The context net's stride-2 convs (core/extractor.py:20-80: 3x3 s2 p1 and the 1x1 s2
+    projection finishing a block as relu(conv + b + y)) as depth-1 volumes on the stride-2 tiles,
+    odd sizes included, vs fp64 torch."""
+    import torch.nn.functional as F
+    gen = torch.Generator().manual_seed(k + cin + H)
+    x = torch.randn(2, cin, H, W, generator=gen)
+    w = torch.randn(cout, cin, k, k, generator=gen) * 0.05
+    bias = torch.randn(cout, generator=gen) * 0.1
+    ref = F.conv2d(x.double(), w.double(), bias.double(), stride=2, padding=k // 2)
+    y = torch.randn(ref.shape, generator=gen) if res else None
+    ref = F.relu(ref + y.double()) if res else F.relu(ref)
+    out = ops_mod.conv3d(g(x).unsqueeze(2), ops_mod.PackedConv(g(w), mode="halo"), bias=g(bias), act="relu",
+                         res=g(y).unsqueeze(2) if res else None, res_pre=res, stride=2).squeeze(2)
+    close(out, ref, atol=2e-5, rtol=1e-5)
+
+
+def test_context_resblock_s2_vs_torch(ops_mod):
+    """ResidualBlock(stride 2, batch norm) fast path (every conv on the halo kernel, the projection
+    fused with the block's final relu(x + y)) vs the same module in fp64 on the CPU."""
+    import copy
+    from foundationstereo_amd.extractor import ResidualBlock
+    m = ResidualBlock(64, 96, "batch", stride=2).eval()
+    synth.init_module_(m, seed=91)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 64, 60, 81, generator=gen)
+    with torch.no_grad():
+        ref = copy.deepcopy(m).double()(x.double())
+        out = m.to(DEV)(x.to(DEV))
+    close(out, ref, atol=5e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("nsplit", [1, 2])
 @pytest.mark.parametrize("kern,stride,cfg", [((17, 1, 1), 1, -1), ((17, 1, 1), 1, 7), ((3, 3, 3), 2, 10),
                                              ((1, 3, 3), 1, 5)])
