@@ -248,7 +248,7 @@ class FoundationStereo(nn.Module):
         md = self.args.get("mixed_dtype", "float16")
         with autocast(mp, md):
             features_left, features_right, vit_feat = self._backbone(image1, image2)
-            stem_2x = self.stem_2(image1)
+            stem_2x = _sub.run_seq(self.stem_2, image1)      # BasicConv_IN s2 + conv3x3 + IN + ReLU
             vol = self.build_stem_volume(features_left[0], features_right[0])
             vol = self.corr_stem[1:](vol)
             vol = self.corr_feature_att(vol, features_left[0])

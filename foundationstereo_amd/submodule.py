@@ -125,6 +125,24 @@ def conv2d_s2_bn_act(x, conv, bn, act=None, res=None, res_pre=False):
     return ops.conv3d(_f32(x).unsqueeze(2), pk, bias=b, act=act, res=r, res_pre=res_pre, stride=2).squeeze(2)
 
 
+def conv_any(conv, x):
+    """conv(x) for a bare (no-norm) Conv2d: stride 1 on the halo kernel, 3x3 s2 / 1x1 s2 on its stride-2
+    tiles, anything else (incl. fp16 output under autocast when the input is fp16) through torch."""
+    if type(conv) is nn.Conv2d:
+        if _fast2d(x, conv, None):
+            return conv2d_bn_act([x], conv, None)
+        if _fast_s2_2d(x, conv, None):
+            return conv2d_s2_bn_act(x, conv, None)
+    return conv(x)
+
+
+def run_seq(seq, x):
+    """nn.Sequential forward with its bare Conv2d layers through ``conv_any``."""
+    for m in seq:
+        x = conv_any(m, x) if type(m) is nn.Conv2d else m(x)
+    return x
+
+
 def _fast_up3d(x, conv, bn) -> bool:
     """ConvTranspose3d(k=4, s=2, p=1) (+ eval BatchNorm3d) that the 2x2x2 phase tiles run."""
     if not (FILTER3D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
@@ -439,7 +457,7 @@ class BasicConv_IN(nn.Module):
         self.IN = nn.InstanceNorm3d(out_channels) if is_3d else nn.InstanceNorm2d(out_channels)
 
     def forward(self, x):
-        x = self.conv(x)
+        x = conv_any(self.conv, x)
         if self.use_in:
             x = self.IN(x)
         return F.leaky_relu(x, 0.01) if self.relu else x
