@@ -19,6 +19,8 @@ is the data path:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -54,6 +56,11 @@ def normalize_image(img):
 
 
 _NORM_CACHE = {}
+
+
+# the context net (+ stem_2, CAM / SAM) and the hourglass's disparity-transformer branch on side
+# streams beside the 3D path (FSMI_CTX_OVERLAP=0: in order on the current stream, for A/B)
+CTX_OVERLAP = os.environ.get("FSMI_CTX_OVERLAP", "1") != "0"
 
 
 def _gated(seq, x, gate):
@@ -109,6 +116,16 @@ class hourglass(nn.Module):
         self.feature_att_up_8 = FeatureAtt(2 * c, feat_dims[1])
 
     def forward(self, x, features):
+        dt_s = None
+        if _update.OVERLAP and CTX_OVERLAP and self._dt_fast(x, x):
+            # the disparity transformer branch (patch embed + 4 encoder layers, ~0.45 ms at cfg2, a few
+            # hundred waves) reads only x: it runs on a side stream beside conv1 .. conv1_up
+            main = torch.cuda.current_stream(x.device)
+            dt_s = _update._side_stream(x.device, 1)
+            dt_s.wait_stream(main)
+            with torch.cuda.stream(dt_s):
+                scale, shift = self._patch_fold()
+                t = self.atts["4"](ops.dt_patch_embed(_sub._f32(x), self.conv_patch[0].weight.float(), scale, shift))
         if _sub.FATT_FUSE and not self.training:
             # each FeatureAtt's sigmoid(gate) * cv in the epilogue of the conv that produces cv
             # (core/foundation_stereo.py:93-109, core/submodule.py:452-453)
@@ -124,6 +141,12 @@ class hourglass(nn.Module):
             c2 = self.feature_att_up_16(self.agg_0(torch.cat((self.conv3_up(c3), c2), dim=1)), features[2])
             c1 = self.feature_att_up_8(self.agg_1(torch.cat((self.conv2_up(c2), c1), dim=1)), features[1])
         conv = self.conv1_up(c1)
+        if dt_s is not None and tuple(conv.shape) == tuple(x.shape):
+            main.wait_stream(dt_s)
+            t.record_stream(main)
+            return self.conv_out(ops.upsample4_add_(conv.float().contiguous(), t))
+        if dt_s is not None:
+            main.wait_stream(dt_s)
         if self._dt_fast(x, conv):
             # patch embed, transformer and the x4 trilinear add on HIP (csrc/transformer.hip)
             scale, shift = self._patch_fold()
@@ -233,6 +256,16 @@ class FoundationStereo(nn.Module):
         out, vit_feat = self.feature(torch.cat([image1, image2], dim=0))
         return [o[:B] for o in out], [o[B:] for o in out], vit_feat[:B]
 
+    def _context(self, image1, vit_feat):
+        """stem_2 and the context features (core/foundation_stereo.py:207,221-226)."""
+        stem_2x = _sub.run_seq(self.stem_2, image1)      # BasicConv_IN s2 + conv3x3 + IN + ReLU
+        cnet_list = self.cnet(image1, vit_feat=vit_feat, num_layers=self.args.n_gru_layers)
+        net_list = [torch.tanh(x[0]) for x in cnet_list]
+        inp_list = [torch.relu(x[1]) for x in cnet_list]
+        inp_list = [self.cam(x) * x for x in inp_list]
+        att = [self.sam(x) for x in inp_list]
+        return stem_2x, net_list, inp_list, att
+
     def upsample_disp(self, disp, mask_feat_4, stem_2x):
         """core/foundation_stereo.py:183-191: returns (B,1,H,W) fp32."""
         with autocast(self.args.mixed_precision, self.args.get("mixed_dtype", "float16")):
@@ -248,10 +281,23 @@ class FoundationStereo(nn.Module):
         md = self.args.get("mixed_dtype", "float16")
         with autocast(mp, md):
             features_left, features_right, vit_feat = self._backbone(image1, image2)
-            stem_2x = _sub.run_seq(self.stem_2, image1)      # BasicConv_IN s2 + conv3x3 + IN + ReLU
+            ctx_s = None
+            if _update.OVERLAP and CTX_OVERLAP and image1.is_cuda and not torch.is_grad_enabled():
+                # stem_2 + context net + CAM / SAM read only the images and vit_feat: a side stream
+                # runs them beside the volume build and the 3D filtering (joined before the loop)
+                main = torch.cuda.current_stream(image1.device)
+                ctx_s = _update._side_stream(image1.device, 0)
+                ctx_s.wait_stream(main)
+                with torch.cuda.stream(ctx_s):
+                    stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
+            else:
+                stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
             vol = self.build_stem_volume(features_left[0], features_right[0])
-            vol = self.corr_stem[1:](vol)
-            vol = self.corr_feature_att(vol, features_left[0])
+            if _sub.FATT_FUSE and not self.training:
+                # corr_feature_att's sigmoid(gate) * vol in the last ResNet block's epilogue
+                vol = _gated(self.corr_stem[1:], vol, self.corr_feature_att.logits(features_left[0]))
+            else:
+                vol = self.corr_feature_att(self.corr_stem[1:](vol), features_left[0])
             vol = self.cost_agg(vol, features_left)
             if init_disp is None:
                 cl = self.classifier
@@ -259,11 +305,10 @@ class FoundationStereo(nn.Module):
                 logits = ops.conv3d_direct(cl[1](cl[0](vol)).float(), head.weight.float(),
                                            head.bias.float()).squeeze(1)
                 init_disp = ops.softmax_regression(logits)
-            cnet_list = self.cnet(image1, vit_feat=vit_feat, num_layers=self.args.n_gru_layers)
-            net_list = [torch.tanh(x[0]) for x in cnet_list]
-            inp_list = [torch.relu(x[1]) for x in cnet_list]
-            inp_list = [self.cam(x) * x for x in inp_list]
-            att = [self.sam(x) for x in inp_list]
+            if ctx_s is not None:
+                main.wait_stream(ctx_s)
+                for t in [stem_2x, *net_list, *inp_list, *att]:
+                    t.record_stream(main)
 
         geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
                                               num_levels=self.args.corr_levels, dx=self.dx)

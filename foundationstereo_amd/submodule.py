@@ -314,12 +314,17 @@ class _ResBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
-    def forward(self, x):
+    def forward(self, x, fatt=None):
+        """``fatt`` (3D blocks): a following FeatureAtt's pre-sigmoid gate, applied in conv2's epilogue
+        (returns sigmoid(fatt).unsqueeze(2) * block(x))."""
         bn1 = self.bn1 if self.norm_layer is not None else None
         bn2 = self.bn2 if self.norm_layer is not None else None
         if self.downsample is None and _fast3d(x, self.conv1, bn1) and _fast3d(x, self.conv2, bn2):
             y = conv3d_bn_act(x, self.conv1, bn1, "relu")
-            return conv3d_bn_act(y, self.conv2, bn2, "relu", res=x, res_pre=True)   # relu(bn2(conv2) + x)
+            # relu(bn2(conv2) + x) [* sigmoid(fatt)]
+            return conv3d_bn_act(y, self.conv2, bn2, "relu", res=x, res_pre=True, fatt=fatt)
+        if fatt is not None:
+            return torch.sigmoid(fatt).unsqueeze(2) * self.forward(x)
         y = self.conv1(x)
         if self.norm_layer is not None:
             y = self.bn1(y)
