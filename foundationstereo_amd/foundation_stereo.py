@@ -115,7 +115,14 @@ class hourglass(nn.Module):
         self.feature_att_up_16 = FeatureAtt(4 * c, feat_dims[2])
         self.feature_att_up_8 = FeatureAtt(2 * c, feat_dims[1])
 
-    def forward(self, x, features):
+    def gate_logits(self, features):
+        """The five FeatureAtt gates (pre-sigmoid), in the order forward uses them."""
+        return (self.feature_att_8.logits(features[1]), self.feature_att_16.logits(features[2]),
+                self.feature_att_32.logits(features[3]), self.feature_att_up_16.logits(features[2]),
+                self.feature_att_up_8.logits(features[1]))
+
+    def forward(self, x, features, gates=None):
+        """``gates``: precomputed ``gate_logits(features)`` (ready on the current stream)."""
         dt_s = None
         if _update.OVERLAP and CTX_OVERLAP and self._dt_fast(x, x):
             # the disparity transformer branch (patch embed + 4 encoder layers, ~0.45 ms at cfg2, a few
@@ -129,11 +136,12 @@ class hourglass(nn.Module):
         if _sub.FATT_FUSE and not self.training:
             # each FeatureAtt's sigmoid(gate) * cv in the epilogue of the conv that produces cv
             # (core/foundation_stereo.py:93-109, core/submodule.py:452-453)
-            c1 = _gated(self.conv1, x, self.feature_att_8.logits(features[1]))
-            c2 = _gated(self.conv2, c1, self.feature_att_16.logits(features[2]))
-            c3 = _gated(self.conv3, c2, self.feature_att_32.logits(features[3]))
-            c2 = _gated(self.agg_0, torch.cat((self.conv3_up(c3), c2), dim=1), self.feature_att_up_16.logits(features[2]))
-            c1 = _gated(self.agg_1, torch.cat((self.conv2_up(c2), c1), dim=1), self.feature_att_up_8.logits(features[1]))
+            g8, g16, g32, gu16, gu8 = gates if gates is not None else self.gate_logits(features)
+            c1 = _gated(self.conv1, x, g8)
+            c2 = _gated(self.conv2, c1, g16)
+            c3 = _gated(self.conv3, c2, g32)
+            c2 = _gated(self.agg_0, torch.cat((self.conv3_up(c3), c2), dim=1), gu16)
+            c1 = _gated(self.agg_1, torch.cat((self.conv2_up(c2), c1), dim=1), gu8)
         else:
             c1 = self.feature_att_8(self.conv1(x), features[1])
             c2 = self.feature_att_16(self.conv2(c1), features[2])
@@ -292,13 +300,33 @@ class FoundationStereo(nn.Module):
                     stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
             else:
                 stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
+            fuse = _sub.FATT_FUSE and not self.training
+            gates = None
+            if fuse and ctx_s is not None:
+                # the six FeatureAtt gates (2D 1x1 convs on the features) on a side stream, ready long
+                # before the volume convs that apply them; an event joins only them
+                g_s = _update._side_stream(image1.device, 1)
+                g_s.wait_stream(main)
+                with torch.cuda.stream(g_s):
+                    gates = (self.corr_feature_att.logits(features_left[0]),) + \
+                        self.cost_agg.gate_logits(features_left)
+                    g_ev = torch.cuda.Event()
+                    g_ev.record(g_s)
             vol = self.build_stem_volume(features_left[0], features_right[0])
-            if _sub.FATT_FUSE and not self.training:
-                # corr_feature_att's sigmoid(gate) * vol in the last ResNet block's epilogue
-                vol = _gated(self.corr_stem[1:], vol, self.corr_feature_att.logits(features_left[0]))
+            if fuse:
+                # corr_feature_att's sigmoid(gate) * vol in the last ResNet block's epilogue; the gates
+                # are joined right before it (~1 ms of volume convs after the fork)
+                for m in list(self.corr_stem)[1:-1]:
+                    vol = m(vol)
+                if gates is not None:
+                    main.wait_event(g_ev)
+                    for t in gates:
+                        t.record_stream(main)
+                g0 = gates[0] if gates is not None else self.corr_feature_att.logits(features_left[0])
+                vol = self.corr_stem[-1](vol, fatt=g0)
             else:
                 vol = self.corr_feature_att(self.corr_stem[1:](vol), features_left[0])
-            vol = self.cost_agg(vol, features_left)
+            vol = self.cost_agg(vol, features_left, gates=None if gates is None else gates[1:])
             if init_disp is None:
                 cl = self.classifier
                 head = cl[2]   # Conv3d(14, 1, 7, padding=3): direct gfx950 kernel (MIOpen: ~1 TFLOP/s here)
