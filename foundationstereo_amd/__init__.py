@@ -9,8 +9,9 @@ import os as _os
 
 __version__ = "0.1.0"
 
-# MIOpen runs the dense convolutions.  Its exhaustive Find benchmarks naive
-# kernels (seconds each for the 3D deconvs) on first use; instead ship the
+# MIOpen runs only the few convs left outside the HIP kernels (the context net's 7x7 s2 stem and
+# 4x4 s4 `down`, the spx ConvTranspose2d pair, CAM / SAM) and every conv of the torch fallback
+# paths.  Its exhaustive Find benchmarks naive kernels (seconds each) on first use; instead ship the
 # find-db measured on MI355X for these layer shapes (tuning/miopen) and use
 # FAST mode: db hit -> tuned solver, miss -> immediate-mode heuristic, never a
 # search.  Both are only defaults; an explicit environment wins.
