@@ -327,6 +327,14 @@ class FoundationStereo(nn.Module):
             else:
                 vol = self.corr_feature_att(self.corr_stem[1:](vol), features_left[0])
             vol = self.cost_agg(vol, features_left, gates=None if gates is None else gates[1:])
+            geo_fn = None
+            if ctx_s is not None:
+                # the geometry pyramids (all-pairs correlation + volume pyramid) beside the classifier
+                geo_s = _update._side_stream(image1.device, 1)
+                geo_s.wait_stream(main)
+                with torch.cuda.stream(geo_s):
+                    geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(),
+                                                          vol.float(), num_levels=self.args.corr_levels, dx=self.dx)
             if init_disp is None:
                 cl = self.classifier
                 head = cl[2]   # Conv3d(14, 1, 7, padding=3): direct gfx950 kernel (MIOpen: ~1 TFLOP/s here)
@@ -338,8 +346,13 @@ class FoundationStereo(nn.Module):
                 for t in [stem_2x, *net_list, *inp_list, *att]:
                     t.record_stream(main)
 
-        geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
-                                              num_levels=self.args.corr_levels, dx=self.dx)
+        if geo_fn is None:
+            geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
+                                                  num_levels=self.args.corr_levels, dx=self.dx)
+        else:
+            main.wait_stream(geo_s)
+            for t in [*geo_fn.init_corr_pyramid, *geo_fn.geo_volume_pyramid]:
+                t.record_stream(main)
         disp = init_disp.float()
         disp_preds = []
         disp_up = None
