@@ -14,6 +14,7 @@
 #include <torch/library.h>
 #include <ATen/core/Tensor.h>
 #include <ATen/ops/empty.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
 #include <vector>
@@ -48,6 +49,7 @@ const float* cp(const Tensor& t) { return t.data_ptr<float>(); }
 float* mp(Tensor& t) { return t.data_ptr<float>(); }
 
 Tensor gwc_volume(const Tensor& fl_, const Tensor& fr_, int64_t maxdisp, int64_t num_groups) {
+  const c10::DeviceGuard guard(fl_.device());   // launch + allocate on the tensors' device
   check_dev("gwc_volume", fl_); check_dev("gwc_volume", fr_);
   TORCH_CHECK(fl_.dim() == 4 && fl_.sizes() == fr_.sizes(), "gwc_volume: fl, fr must be (B,C,H,W) alike");
   Tensor fl = dense(fl_), fr = dense(fr_);
@@ -58,6 +60,7 @@ Tensor gwc_volume(const Tensor& fl_, const Tensor& fr_, int64_t maxdisp, int64_t
 }
 
 Tensor concat_volume(const Tensor& pl_, const Tensor& pr_, int64_t maxdisp) {
+  const c10::DeviceGuard guard(pl_.device());
   check_dev("concat_volume", pl_); check_dev("concat_volume", pr_);
   TORCH_CHECK(pl_.dim() == 4 && pl_.sizes() == pr_.sizes(), "concat_volume: pl, pr must be (B,C,H,W) alike");
   Tensor pl = dense(pl_), pr = dense(pr_);
@@ -68,6 +71,7 @@ Tensor concat_volume(const Tensor& pl_, const Tensor& pr_, int64_t maxdisp) {
 }
 
 std::vector<Tensor> allpairs_corr(const Tensor& fl_, const Tensor& fr_, int64_t num_levels) {
+  const c10::DeviceGuard guard(fl_.device());
   check_dev("allpairs_corr", fl_); check_dev("allpairs_corr", fr_);
   TORCH_CHECK(fl_.dim() == 4 && fl_.sizes() == fr_.sizes(), "allpairs_corr: fl, fr must be (B,C,H,W) alike");
   TORCH_CHECK(num_levels >= 1 && num_levels <= 8, "allpairs_corr: num_levels in [1,8]");
@@ -86,6 +90,7 @@ std::vector<Tensor> allpairs_corr(const Tensor& fl_, const Tensor& fr_, int64_t 
 }
 
 std::vector<Tensor> volume_pyramid(const Tensor& vol_, int64_t num_levels) {
+  const c10::DeviceGuard guard(vol_.device());
   check_dev("volume_pyramid", vol_);
   TORCH_CHECK(vol_.dim() == 5, "volume_pyramid: vol must be (B,Cv,D,H,W)");
   TORCH_CHECK(num_levels >= 1 && num_levels <= 8, "volume_pyramid: num_levels in [1,8]");
@@ -106,6 +111,7 @@ Tensor geo_lookup(at::TensorList vol_levels, at::TensorList corr_levels, const T
   const int64_t L = vol_levels.size();
   TORCH_CHECK(L >= 1 && L <= 8 && (int64_t)corr_levels.size() == L, "geo_lookup: 1..8 levels of each pyramid");
   check_dev("geo_lookup", disp_);
+  const c10::DeviceGuard guard(disp_.device());
   const Tensor& v0 = vol_levels[0];
   TORCH_CHECK(v0.dim() == 5, "geo_lookup: volume levels must be (B,Cv,D,H,W)");
   const int64_t B = v0.size(0), Cv = v0.size(1), D = v0.size(2), H = v0.size(3), W = v0.size(4);
@@ -131,6 +137,7 @@ Tensor geo_lookup(at::TensorList vol_levels, at::TensorList corr_levels, const T
 }
 
 Tensor bilinear_sampler_1d(const Tensor& img_, const Tensor& x_) {
+  const c10::DeviceGuard guard(img_.device());
   check_dev("bilinear_sampler", img_); check_dev("bilinear_sampler", x_);
   TORCH_CHECK(img_.dim() == 4 && img_.size(2) == 1, "bilinear_sampler_1d: img must be (P,C,1,Lx)");
   const int64_t P = img_.size(0), C = img_.size(1), Lx = img_.size(3), K = x_.size(-1);
@@ -142,6 +149,7 @@ Tensor bilinear_sampler_1d(const Tensor& img_, const Tensor& x_) {
 }
 
 Tensor disparity_regression(const Tensor& prob_, int64_t maxdisp) {
+  const c10::DeviceGuard guard(prob_.device());
   check_dev("disparity_regression", prob_);
   TORCH_CHECK(prob_.dim() == 4 && prob_.size(1) == maxdisp, "disparity_regression: prob must be (B,maxdisp,H,W)");
   Tensor prob = dense(prob_);
@@ -152,6 +160,7 @@ Tensor disparity_regression(const Tensor& prob_, int64_t maxdisp) {
 }
 
 Tensor softmax_regression(const Tensor& logits_) {
+  const c10::DeviceGuard guard(logits_.device());
   check_dev("softmax_regression", logits_);
   TORCH_CHECK(logits_.dim() == 4, "softmax_regression: logits must be (B,D,H,W)");
   Tensor logits = dense(logits_);
@@ -162,6 +171,7 @@ Tensor softmax_regression(const Tensor& logits_) {
 }
 
 Tensor context_upsample(const Tensor& disp_, const Tensor& w_) {
+  const c10::DeviceGuard guard(disp_.device());
   check_dev("context_upsample", disp_); check_dev("context_upsample", w_);
   TORCH_CHECK(disp_.dim() == 4 && disp_.size(1) == 1, "context_upsample: disp_low must be (B,1,h,w)");
   const int64_t B = disp_.size(0), h = disp_.size(2), w = disp_.size(3);
@@ -173,6 +183,7 @@ Tensor context_upsample(const Tensor& disp_, const Tensor& w_) {
 }
 
 Tensor softmax_context_upsample(const Tensor& disp_, const Tensor& logits_, double scale) {
+  const c10::DeviceGuard guard(disp_.device());
   check_dev("softmax_context_upsample", disp_); check_dev("softmax_context_upsample", logits_);
   TORCH_CHECK(disp_.dim() == 4 && disp_.size(1) == 1, "softmax_context_upsample: disp_low must be (B,1,h,w)");
   const int64_t B = disp_.size(0), h = disp_.size(2), w = disp_.size(3);
@@ -191,7 +202,8 @@ TORCH_LIBRARY(fsmi, m) {
   m.def("gwc_volume(Tensor fl, Tensor fr, int maxdisp, int num_groups) -> Tensor");
   m.def("concat_volume(Tensor pl, Tensor pr, int maxdisp) -> Tensor");
   m.def("allpairs_corr(Tensor fl, Tensor fr, int num_levels) -> Tensor[]");
-  m.def("volume_pyramid(Tensor vol, int num_levels) -> Tensor[]");
+  // level 0 IS `vol` (the reference keeps the filtered volume as its level 0, core/geometry.py:29-36)
+  m.def("volume_pyramid(Tensor(a -> *) vol, int num_levels) -> Tensor(a)[]");
   m.def("geo_lookup(Tensor[] vol_levels, Tensor[] corr_levels, Tensor disp, int radius) -> Tensor");
   m.def("bilinear_sampler_1d(Tensor img, Tensor x) -> Tensor");
   m.def("disparity_regression(Tensor prob, int maxdisp) -> Tensor");

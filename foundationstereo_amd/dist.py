@@ -93,11 +93,13 @@ class ShardedStereo:
         self.world = world
         self._local = None          # this rank's shard, (b, 2, 3, H, W), fixed storage
         self._graph = None          # (hipGraph, static output) after capture()
+        self._dtype_checked = False
 
     def _local_buffer(self, batch):
         b = batch.shape[0] // self.world
         shape = (b,) + tuple(batch.shape[1:])
-        if self._local is None or tuple(self._local.shape) != shape or self._local.device != batch.device:
+        if (self._local is None or tuple(self._local.shape) != shape or self._local.device != batch.device
+                or self._local.dtype != batch.dtype):
             self._local = torch.empty(shape, device=batch.device, dtype=batch.dtype)
             self._graph = None
         return self._local
@@ -109,6 +111,16 @@ class ShardedStereo:
             local.copy_(batch)
             return local
         host = _host_staged()
+        if not self._dtype_checked:
+            # non-zero ranks pass a placeholder: its dtype must be rank 0's or the scatter mismatches
+            codes = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.uint8]
+            assert batch.dtype in codes, f"unsupported batch dtype {batch.dtype}"
+            code = torch.tensor([codes.index(batch.dtype)], dtype=torch.int64,
+                                device="cpu" if host else batch.device)
+            dist.broadcast(code, src=0)
+            if codes[int(code.item())] != batch.dtype:
+                raise TypeError(f"rank {self.rank}: batch dtype {batch.dtype} != rank 0's {codes[int(code.item())]}")
+            self._dtype_checked = True
         chunks = None
         if self.rank == 0:
             chunks = list((batch.cpu() if host else batch).chunk(self.world, 0))

@@ -340,6 +340,12 @@ class PackedConv:
         if hit is None:
             b = torch.zeros_like(self.wscale) if bias is None else bias.detach().float().reshape(-1)
             assert b.numel() == self.cout, f"bias of {b.numel()} for {self.cout} output channels"
+            if bias is not None and not isinstance(bias, torch.nn.Parameter):
+                # a per-call temporary (e.g. bias.float() under a half model): keep only the latest
+                # such entry so the cache stays bounded; parameters are bounded by the module tree
+                for k in [k for k, v in self._sb.items() if v[1] is not None
+                          and not isinstance(v[1], torch.nn.Parameter)]:
+                    del self._sb[k]
             hit = self._sb[key] = (torch.stack([self.wscale, b], 1).contiguous(), bias)
         return hit[0]
 

@@ -14,7 +14,6 @@ recompiles.  Like ``ops``, there is no CPU kernel: CPU tensors raise.
 from __future__ import annotations
 
 import os
-import shutil
 
 from .build import LIB, LIB_DIR, PKG, build_library
 
@@ -28,8 +27,14 @@ OPS = ("gwc_volume", "concat_volume", "allpairs_corr", "volume_pyramid", "geo_lo
 
 
 def build_extension(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/torch_ops.cpp with torch.utils.cpp_extension into _lib/fsmi_torch.so."""
-    import torch
+    """Compile csrc/torch_ops.cpp into _lib/fsmi_torch.so.
+
+    The compile and link run as plain subprocesses with the include / library paths
+    torch.utils.cpp_extension reports, and nothing is loaded into the building process:
+    ``cpp_extension.load`` would dlopen its build/ copy and register ``TORCH_LIBRARY(fsmi)``,
+    and a later ``load()`` of the _lib copy would register the namespace a second time (a
+    c10::Error thrown from a static constructor aborts the process)."""
+    import subprocess
     from torch.utils import cpp_extension
 
     lib = build_library()
@@ -37,19 +42,40 @@ def build_extension(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(EXT) and all(os.path.getmtime(d) <= os.path.getmtime(EXT) for d in deps):
         return EXT
     os.makedirs(_BUILD_DIR, exist_ok=True)
-    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
-    so = cpp_extension.load(
-        name="fsmi_torch", sources=[SRC], build_directory=_BUILD_DIR, is_python_module=False,
-        extra_include_paths=["/opt/rocm/include"],
-        extra_cflags=["-O2", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1"],
-        # ninja turns '$$' into '$' and the quotes keep the shell off it; the second runpath entry
-        # lets cpp_extension import the copy it links under build/ before it sits next to libfsmi.so
-        extra_ldflags=[f"-L{tlib}", "-lc10_hip", f"-L{LIB_DIR}", "-lfsmi",
-                       "-Wl,-rpath,'$$ORIGIN:$$ORIGIN/../../foundationstereo_amd/_lib'"],
-        verbose=verbose)
-    del so
-    shutil.copy2(os.path.join(_BUILD_DIR, "fsmi_torch.so"), EXT)
+    obj = os.path.join(_BUILD_DIR, "torch_ops.o")
+    tmp = os.path.join(_BUILD_DIR, "fsmi_torch.so")
+    incs = [f"-I{d}" for d in cpp_extension.include_paths("cuda")]
+    libs = [f"-L{d}" for d in cpp_extension.library_paths("cuda")]
+    cxx = os.environ.get("CXX", "c++")
+    cmds = [
+        [cxx, "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
+         *incs, "-c", SRC, "-o", obj],
+        # $ORIGIN: the .so sits next to libfsmi.so in _lib/
+        [cxx, "-shared", obj, "-o", tmp, *libs, f"-L{LIB_DIR}", "-lfsmi", "-lc10_hip", "-lc10", "-ltorch_cpu",
+         "-ltorch", "-Wl,-rpath,$ORIGIN"],
+    ]
+    for cmd in cmds:
+        if verbose:
+            print(" ".join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"torch_ops build failed ({' '.join(cmd)}):\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, EXT)
     return EXT
+
+
+def _registered() -> bool:
+    import torch
+    try:
+        torch.ops.fsmi.gwc_volume        # resolves only once TORCH_LIBRARY(fsmi) has run
+        return True
+    except (AttributeError, RuntimeError):
+        return False
+
+
+def available() -> bool:
+    """Whether the operator library is built (or already registered in this process)."""
+    return _loaded or os.path.exists(EXT)
 
 
 def load() -> None:
@@ -63,7 +89,8 @@ def load() -> None:
                            "(or __graft_entry__.build())")
     if not os.path.exists(LIB):
         raise RuntimeError(f"{LIB} missing")
-    torch.ops.load_library(EXT)
+    if not _registered():                # a second TORCH_LIBRARY(fsmi) registration aborts
+        torch.ops.load_library(EXT)
     _loaded = True
 
 

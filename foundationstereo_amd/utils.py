@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from . import torch_ops
+from . import ops, torch_ops
 
 
 class InputPadder:
@@ -51,7 +51,10 @@ def bilinear_sampler(img, coords, mode="bilinear", mask=False, low_memory=False,
     P = img.shape[0]
     x = coords[..., 0].reshape(P, -1).float()
     img = img.float()
-    out = torch_ops.op("bilinear_sampler_1d", img, x)(img, x)
+    if torch_ops.available():
+        out = torch_ops.op("bilinear_sampler_1d", img, x)(img, x)
+    else:                                # same kernel over the ctypes front end (libfsmi.so alone)
+        out = ops.bilinear_sampler_1d(img, x)
     out = out.reshape(P, img.shape[1], 1, -1)
     if mask:
         xg = 2 * x / (W - 1) - 1
