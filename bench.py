@@ -290,6 +290,8 @@ def main():
                   else "f32 (3xfp16 split MFMA)"),
         "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
         "range_overflow": range_overflow,
+        # forwards re-run in safe range mode after their range flag came back set (ops.guarded)
+        "range_recoveries": ops.RANGE_RECOVERIES[0],
         "config": {"workload": f"{a.config}: {W}x{H}{' hierarchical' if a.config in HIERA else ''}, "
                                f"max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",

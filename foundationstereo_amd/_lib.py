@@ -61,6 +61,8 @@ SIGNATURES = {
     "fsmi_upsample4_add": [_P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_debug_conv_timestamps": [_P],
     "fsmi_range_status": [_I, ctypes.POINTER(_I)],
+    "fsmi_set_range_safe": [_I],
+    "fsmi_get_range_safe": [ctypes.POINTER(_I)],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],

@@ -678,6 +678,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   else hs.load(a, tc.b, cc_begin);
   int sx = kNoExp;                 // block exponent of the split (see chunk_exp)
   bool ovf = false;
+  constexpr bool m1 = RM == 1;     // per-chunk exponent (mode 1)
   for (int cc = cc_begin; cc < cc_end; ++cc) {
     if constexpr (RM == 3) {
       const float lm = hs.absmax();
@@ -687,7 +688,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
       } else {
         range3_check(rflag, lm, sx, lane, wave);
       }
-    } else if (RM == 1 || (RM == 2 && cc == cc_begin)) {
+    } else if (m1 || (RM == 2 && sx == kNoExp)) {
       const float m = wave_max(hs.absmax());
       if (lane == 0) red[wave] = m;           // m is wave-uniform (SGPR)
     }
@@ -709,7 +710,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
           sx = se;
         }
       }
-    } else if constexpr (RM == 1) {
+    } else if (m1) {
       const float bm = red4_max(red);
       ovf |= !(bm <= 3.4e38f);                  // an inf input (NaN is ignored by the max)
       // rescale only when the chunk does not fit the current exponent; then re-aim with headroom
@@ -719,8 +720,8 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
         if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
         sx = se;
       }
-    } else if constexpr (RM == 2) {
-      if (cc == cc_begin) sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
+    } else if (RM == 2 && sx == kNoExp) {       // first chunk with a nonzero value
+      sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
     }
     hs.template store<RM>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
     if (cc + 1 < cc_end) {
@@ -873,19 +874,22 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
     };
     int sx = kNoExp;               // block (group) exponent of the segment (see chunk_exp)
     bool ovf = false;
+    constexpr bool m1 = RM == 1;     // per-chunk exponent (mode 1)
     // q-th chunk of this group (cc = c_first + KG q); both groups run the same number of stages
     // (barriers), a group past its last chunk idles through them
     auto stage = [&](int q) FSMI_HALO_INL {
       const int cc = c_first + KG * q;
       const bool valid = q < n_g;
-      if (valid && (RM == 1 || (RM == 2 && q == 0))) {
+      // mode 2 fixes the exponent at the first chunk holding a nonzero value (an all-zero first
+      // chunk would otherwise leave scale 1 and drop small later values to fp16 subnormals)
+      if (valid && (m1 || (RM == 2 && sx == kNoExp))) {
         const float m = wave_max(hs.absmax());
         if (lane == 0) gred[wave] = m;          // m is wave-uniform (SGPR)
       }
       __syncthreads();             // every wave is done with the previous chunk's halo; maxima visible
       if (tsb && threadIdx.x == 0 && q < 36) tsb[1 + q] = wall_clock64();
       if (valid) {
-        if constexpr (RM == 1) {
+        if (m1) {
           const float bm = red4_max(gred);
           ovf |= !(bm <= 3.4e38f);              // an inf input (NaN is ignored by the max)
           // rescale only when the chunk does not fit the current exponent; then re-aim with headroom
@@ -894,8 +898,8 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
             if (sx != kNoExp) rescale_acc<TM, TN>(acc, exp2i(se - sx));
             sx = se;
           }
-        } else if constexpr (RM == 2) {
-          if (q == 0) sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(gred)));
+        } else if (RM == 2 && sx == kNoExp) {
+          sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(gred)));
         }
         hs.template store<RM>(gXh, gXl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
         if (cc + KG < cc_end && !(a.dbg & 2)) {

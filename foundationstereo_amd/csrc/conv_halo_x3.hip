@@ -153,7 +153,14 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     else if (KS == 3) cfg = Cout > 64 ? 3 : (a.Cin <= 64 ? 5 : 2);
     else cfg = Cout > 64 ? 4 : 5;
   }
-  const bool d3 = D > 1 || KD > 1;
+  bool d3 = D > 1 || KD > 1;
+  if (!d3 && range_safe()) {
+    // safe range mode: the volume instantiation (range mode 1: per-chunk block exponent with exact
+    // accumulator rescaling) with D = KD = 1 is the same 2D conv; the pointwise tiles (mode 2 only)
+    // take the 128 x 2 x 32 register-weight tile
+    d3 = true;
+    if (cfg >= 24) cfg = 4;
+  }
   const bool pw = cfg >= 24;
   if (pw) {                                        // pointwise LDS-DMA tiles (conv_pw.hip)
     FSMI_CHECK_ARG(cfg <= 26 && KS == 1 && !d3 && HW % 4 == 0, "%s: pointwise tile %d needs a 2D 1x1 conv with "

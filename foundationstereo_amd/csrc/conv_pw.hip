@@ -145,7 +145,9 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
     wait_vmcnt<2 * OPS + 4 * TM>();                // this wave's part of chunk q has landed
     bar();                                         // ... and every wave's
     const float* xs = ring[q % NS];
-    if (q == 0) {                                  // block exponent from the first chunk (range mode 2)
+    // block exponent (range mode 2) from the first chunk holding a nonzero value (an all-zero first
+    // chunk would leave scale 1 and drop small later values to fp16 subnormals)
+    if (sx == kNoExp) {
       float m = 0.f;
 #pragma unroll
       for (int u = 0; u < CHF / 1024; ++u) {

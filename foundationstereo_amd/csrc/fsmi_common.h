@@ -55,6 +55,9 @@ void set_replay(int kernel, hipStream_t stream, std::function<void()> fn);
 // a scaled activation left fp16's range.  Read / reset by fsmi_range_status.  nullptr if the
 // allocation failed (the kernels then skip the flag).
 int* range_flag_device();
+// Safe range mode (fsmi_set_range_safe): 2D convs take a per-chunk exponent (mode 1) instead of
+// one fixed from the first nonzero chunk; read when a launch's arguments are built.
+int range_safe();
 
 __device__ __forceinline__ long long clock_wave_id() {
   const long long blk = blockIdx.x + static_cast<long long>(gridDim.x) * (blockIdx.y + static_cast<long long>(gridDim.y) * blockIdx.z);

@@ -95,7 +95,10 @@ namespace {
 std::mutex g_range_mu;
 int* g_range_host = nullptr;
 int* g_range_dev = nullptr;
+int g_range_safe = 0;
 }  // namespace
+
+int range_safe() { return __atomic_load_n(&g_range_safe, __ATOMIC_RELAXED); }
 
 int* range_flag_device() {
   std::lock_guard<std::mutex> lk(g_range_mu);
@@ -219,6 +222,17 @@ int fsmi_range_status(int reset, int* overflowed) {
   std::lock_guard<std::mutex> lk(fsmi::g_range_mu);
   *overflowed = __atomic_load_n(fsmi::g_range_host, __ATOMIC_ACQUIRE);
   if (reset) __atomic_store_n(fsmi::g_range_host, 0, __ATOMIC_RELEASE);
+  return FSMI_OK;
+}
+
+int fsmi_set_range_safe(int safe) {
+  __atomic_store_n(&fsmi::g_range_safe, safe ? 1 : 0, __ATOMIC_RELAXED);
+  return FSMI_OK;
+}
+
+int fsmi_get_range_safe(int* safe) {
+  FSMI_CHECK_ARG(safe, "fsmi_get_range_safe: null pointer");
+  *safe = fsmi::range_safe();
   return FSMI_OK;
 }
 

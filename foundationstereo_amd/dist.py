@@ -22,6 +22,9 @@ from typing import Callable, Tuple
 import torch
 import torch.distributed as dist
 
+from . import foundation_stereo as _fs
+from . import ops
+
 
 def env_world() -> Tuple[int, int, int]:
     """(rank, local_rank, world_size) from the torchrun environment (defaults: single process)."""
@@ -143,10 +146,25 @@ class ShardedStereo:
         self._graph = (g, out)
 
     def _run(self, local):
-        if self._graph is not None:
-            self._graph[0].replay()
+        if self._graph is None:
+            return self.fn(local[:, 0], local[:, 1])      # an eager FoundationStereo guards itself
+        self._graph[0].replay()
+        if not (local.is_cuda and _fs.RANGE_GUARD):
             return self._graph[1]
-        return self.fn(local[:, 0], local[:, 1])
+        # range guard once per replay (one synchronisation): a replay whose flag came back set is
+        # recomputed eagerly in safe range mode, and the graph re-captured in that mode
+        if not ops.range_overflowed(reset=True):
+            return self._graph[1]
+        ops.set_range_safe(True)
+        ops.RANGE_RECOVERIES[0] += 1
+        out = self.fn(local[:, 0], local[:, 1]).clone()
+        ops.check_range()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            gout = self.fn(local[:, 0], local[:, 1])
+        self._graph = (g, gout)
+        return out
 
     def step(self, batch: torch.Tensor, out_shape_per_pair: Tuple[int, ...]) -> torch.Tensor:
         B = batch.shape[0]

@@ -61,6 +61,9 @@ _NORM_CACHE = {}
 # the context net (+ stem_2, CAM / SAM) and the hourglass's disparity-transformer branch on side
 # streams beside the 3D path (FSMI_CTX_OVERLAP=0: in order on the current stream, for A/B)
 CTX_OVERLAP = os.environ.get("FSMI_CTX_OVERLAP", "1") != "0"
+# range guard of the split-precision convs, enforced per eager forward (see forward); FSMI_RANGE_GUARD=0
+# leaves the flag to the caller (ops.check_range)
+RANGE_GUARD = os.environ.get("FSMI_RANGE_GUARD", "1") != "0"
 
 
 def _gated(seq, x, gate):
@@ -282,6 +285,17 @@ class FoundationStereo(nn.Module):
         return ops.softmax_context_upsample(disp.float(), logits.float(), 4.0).unsqueeze(1)
 
     def forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):
+        """core/foundation_stereo.py:194-254.  On a HIP device outside graph capture the range guard
+        of the split-precision convs is enforced here, once per forward: the flag is read after the
+        forward (one synchronisation) and a forward that overflowed is re-run in safe range mode
+        (ops.guarded) -- no disparity computed past the flag is returned."""
+        def run():
+            return self._forward(image1, image2, iters, flow_init, test_mode, low_memory, init_disp)
+        if image1.is_cuda and RANGE_GUARD and not torch.cuda.is_current_stream_capturing():
+            return ops.guarded(run)
+        return run()
+
+    def _forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):
         B = len(image1)
         image1 = normalize_image(image1)
         image2 = normalize_image(image2)

@@ -810,6 +810,46 @@ def check_range():
                          "exponent (inputs spanning > 2^9 within one conv tile)")
 
 
+def reset_range_flag():
+    """Clear the range flag without synchronising (kernels still in flight may set it again)."""
+    import ctypes
+    flag = ctypes.c_int(0)
+    _lib.check(_lib.load().fsmi_range_status(1, ctypes.byref(flag)), "range_status")
+
+
+def set_range_safe(safe: bool = True):
+    """Safe range mode for every 2D split-precision conv launched or captured afterwards: a
+    per-chunk block exponent with exact accumulator rescaling (cannot overflow; ~3 % slower)."""
+    _lib.check(_lib.load().fsmi_set_range_safe(1 if safe else 0), "set_range_safe")
+
+
+def range_safe() -> bool:
+    import ctypes
+    v = ctypes.c_int(0)
+    _lib.check(_lib.load().fsmi_get_range_safe(ctypes.byref(v)), "get_range_safe")
+    return bool(v.value)
+
+
+# forwards re-run in safe mode after their range flag came back set (FoundationStereo.forward,
+# ShardedStereo.step); read by tests and the bench
+RANGE_RECOVERIES = [0]
+
+
+def guarded(run):
+    """Run ``run()`` (a whole forward, eager or a graph replay) and return its result, enforcing
+    the range guard once per call: synchronise, read the flag; when it is set, switch to safe
+    range mode (sticky: the activations that overflowed once will again) and run again.  A
+    flag still set in safe mode raises RangeError (an inf / NaN input)."""
+    reset_range_flag()
+    out = run()
+    if range_overflowed(reset=True):
+        set_range_safe(True)
+        RANGE_RECOVERIES[0] += 1
+        out = run()
+        check_range()
+    return out
+
+
 # ---------------------------------------------------------------- timing
 
 # algorithmic fp32 conv FLOPs (2*Cin*Cout*k*k*B*H*W) of the conv2d calls made since the last

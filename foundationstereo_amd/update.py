@@ -437,7 +437,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         gru08(t) and before gru16(t+1) is enqueued, so gru04(t) waits for the former only.  The
         mask head shares the motion stream.  A tensor read on another stream is freed only after
         the freeing stream has joined the reader, so the caching allocator never recycles memory
-        a pending kernel still reads.  Returns (net, mask, disp); mask is the last iteration's."""
+        a pending kernel still reads.  Returns (net, mask, disp); the mask head runs in the last
+        iteration only (test mode discards the others)."""
         dev = disp.device
         main = torch.cuda.current_stream(dev)
         s_mot, s_gru = _side_stream(dev, 0), _side_stream(dev, 3)
@@ -480,9 +481,12 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 with torch.cuda.stream(s_gru):           # gru08(t+1), beside the heads + motion(t+1)
                     n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1))
                 _BRANCH[0] = 1
-            s_mot.wait_stream(main)
-            with torch.cuda.stream(s_mot):
-                mask = _conv(self.mask[2], [_conv(self.mask[0], [n0], "relu")], "relu", alpha=0.25)
+            if t + 1 == iters:
+                # test mode upsamples only the last iteration's disparity: the reference computes the
+                # mask head every iteration and discards all but the last (core/foundation_stereo.py:243-244)
+                s_mot.wait_stream(main)
+                with torch.cuda.stream(s_mot):
+                    mask = _conv(self.mask[2], [_conv(self.mask[0], [n0], "relu")], "relu", alpha=0.25)
             if t + 1 < iters and HEAD_INPLACE:
                 enc = disp.new_empty(B, nc + 1, H, W)
                 self.disp_head(n0, res=disp, out=enc, co0=nc)

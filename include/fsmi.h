@@ -325,6 +325,13 @@ enum {
  * the flag (1 once any conv since the last reset overflowed); reset != 0 clears it.  The flag
  * is written asynchronously: synchronise the streams that ran the convs before reading it. */
 int fsmi_range_status(int reset, int* overflowed);
+/* Safe range mode: while set, every split-precision 2D conv launched (or captured) afterwards takes
+ * a per-chunk block exponent with exact accumulator rescaling (the volumes' mode), which cannot
+ * overflow; ~3 % slower.  FoundationStereo.forward switches it on and re-runs a forward whose
+ * range flag came back set (the reference has no such mode: its convs are fp32 / fp16 autocast,
+ * core/update.py:83-159).  Sticky until cleared. */
+int fsmi_set_range_safe(int safe);
+int fsmi_get_range_safe(int* safe);
 
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
