@@ -62,6 +62,7 @@ SIGNATURES = {
     "fsmi_debug_conv_timestamps": [_P],
     "fsmi_range_status": [_I, ctypes.POINTER(_I)],
     "fsmi_set_range_safe": [_I],
+    "fsmi_range_poison": [_P, ctypes.c_longlong, _P],
     "fsmi_get_range_safe": [ctypes.POINTER(_I)],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],

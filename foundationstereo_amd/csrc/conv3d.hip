@@ -23,7 +23,10 @@ __global__ __launch_bounds__(256) void conv3d_direct_kernel(const float* __restr
   constexpr int P = KS / 2;
   constexpr int ID = kTD + KS - 1, IH = kTH + KS - 1, IW = kTW + KS - 1;
   __shared__ float tile[ID * IH * IW];
-  int bid = blockIdx.x;
+  // XCD-aware order: consecutive tiles (w fastest, then h, then d) on one XCD, so the halos a tile
+  // shares with its neighbours are L2 hits there (the round-robin default put every neighbour on
+  // another XCD's L2: 7.3x the input fetched per launch)
+  int bid = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   const int tw = bid % nTw; bid /= nTw;
   const int th = bid % nTh; bid /= nTh;
   const int td = bid % nTd;

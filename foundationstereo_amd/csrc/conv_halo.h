@@ -98,6 +98,7 @@ struct HaloArgs {
   float* grh;                      // sigmoid(r_pre) * h, written by act 3
   int gHd;
   int* ovf;                        // range flag (host-mapped; set to 1 when a scaled value overflows fp16)
+  int pipe;                        // 2D register-weight tiles: the pipelined-staging variant (cfg 32 + c)
   // transposed-conv phase launches (fsmi_conv3d_up2_halo_x3; all 0 otherwise): the input window
   // shifted by (sd, sh, sw) in {0, 1}, and output voxel (d, h, w) written at (2d + od, 2h + oh,
   // 2w + ow) of the (2D, 2H, 2W) output, whose channel stride is ocstride
@@ -131,6 +132,9 @@ int launch_s2(int ks, int cfg, const HaloArgs& a, hipStream_t s);
 // split-K reduce pass over a.ws (conv_halo_x3.hip)
 void split_reduce(const HaloArgs& a, hipStream_t s);
 void pw_tile(int cfg, HaloArgs& a);
+// depth-blocked (17, 1, 1) volume tile (cfg 30, conv_depth.hip)
+bool depth_conv_ok(const HaloArgs& a);
+int launch_depth(HaloArgs& a, hipStream_t s);
 
 // tiles with an in-block K-group (kg = 2) instantiation: the register-weight tiles that fit two
 // waves per SIMD (<= 256 VGPRs) with 512-thread blocks
@@ -996,9 +1000,145 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
 }
 
+// ---------------------------------------------------------------- cfg 32 + c: pipelined staging
+
+// Tile c of the register-weight kernel for 2D maps (KG = 1, stride 1) with the next chunk's
+// staging moved into the MFMA stream.  conv_halo_wreg_kernel stages a chunk between two barriers
+// while the MFMA pipes idle: load (one chunk ahead) -> barrier -> split fp32 into fp16 hi / lo and
+// store to LDS -> barrier -> 9 taps of MFMAs.  Here the halo is double-buffered in LDS: while the
+// waves run chunk q's taps on buffer q & 1, the split + store of chunk q + 1 (its registers loaded
+// during chunk q - 1) into buffer (q + 1) & 1 is issued after tap 0 (the VALU work co-issues
+// between MFMAs, MI355X_MICROARCH.md: ~5 single-issue instructions hide per 32x32x16 MFMA gap), the
+// loads of chunk q + 2 follow it, and ONE barrier closes the chunk.  Range mode 2 as the wreg
+// kernel: the exponent comes from the first chunk with a nonzero value (a chunk that is still all
+// zero takes one extra block-wide max + barrier, block-uniform and rare).  LDS: twice the halo
+// (65 KB for TR = 4, 109 KB for TR = 8).
+template <int KS, int BM, int TR, int WM>
+__global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM / 32, TN = TR / WN;
+  constexpr int NTAP = KS * KS;
+  constexpr int STAGE_TAP = NTAP > 1 ? 1 : 0;      // the tap whose MFMAs cover the next chunk's store
+  using HS = HaloStage<KS, TR>;
+  constexpr int RM = range_mode<false>();
+  static_assert(RM == 2 || RM == 0, "pipelined tiles: range mode 2 (or none)");
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[2][HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[2][HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) float red[4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int hsel = lane >> 5, rl = lane & 31;
+  const int nck = a.CinP / HKC;
+  const TileCoord tc = decode_tile<BM, TR, false>(a, blockIdx.x, gridDim.x);
+  const int c_first = tc.split * a.kpc;
+  const int c_end = min(nck, c_first + a.kpc);
+  const int n = c_end - c_first;                   // >= 1: no empty splits (run_halo)
+
+  int wrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) wrow[i] = min(tc.m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
+  half8 wf[2][TM][2][2];           // [buffer][i][k half][hi, lo]
+  auto load_wf = [&](auto buf_c, int cc, int tap) FSMI_HALO_INL {
+    constexpr int buf = decltype(buf_c)::value;
+    const size_t base = (static_cast<size_t>(tap) * nck + cc) * a.CoutP * HKC;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
+        wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+      }
+  };
+  HS hs;
+  hs.init(a, tid, tc.r0, tc.c0);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  int sx = kNoExp;
+  bool ovf = false;
+  auto scale = [&]() FSMI_HALO_INL { return RM == 2 ? exp2i(sx == kNoExp ? 0 : sx) : 1.f; };
+  auto fix_exponent = [&]() FSMI_HALO_INL {        // block-wide max of the registers' chunk -> sx
+    const float m = wave_max(hs.absmax());
+    if (lane == 0) red[wave] = m;
+    __syncthreads();
+    sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
+  };
+  // prologue: chunk 0 -> buffer 0 (its max fixes the exponent), chunk 1 into registers
+  load_wf(std::integral_constant<int, 0>(), c_first, 0);
+  hs.load(a, tc.b, c_first);
+  if (RM == 2) fix_exponent();
+  hs.template store<RM>(Xh[0], Xl[0], tid, scale(), ovf);
+  if (n > 1) hs.load(a, tc.b, c_first + 1);
+  __syncthreads();
+
+  // chunk q on buffer P = q & 1; tap t uses weight buffer (t + PP) & 1 and prefetches tap t + 1
+  auto chunk = [&](auto par_c, int q) FSMI_HALO_INL {
+    constexpr int P = decltype(par_c)::value;
+    constexpr int PP = (NTAP & 1) ? P : 0;
+    const int cc = c_first + q;
+#pragma unroll
+    for (int tap = 0; tap < NTAP; ++tap) {
+      const bool last = tap + 1 == NTAP;
+      if (((tap + PP) & 1) == 0) {
+        load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, c_end - 1) : cc, last ? 0 : tap + 1);
+      } else {
+        load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, c_end - 1) : cc, last ? 0 : tap + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (tap == STAGE_TAP && q + 1 < n) {
+        // next chunk: registers (loaded one chunk ago) -> fp16 hi / lo -> the other buffer, then the
+        // chunk after it into the registers
+        if (RM == 2 && sx == kNoExp) fix_exponent();   // every chunk so far all zero (uniform)
+        hs.template store<RM>(Xh[P ^ 1], Xl[P ^ 1], tid, scale(), ovf);
+        if (q + 2 < n) hs.load(a, tc.b, cc + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int dh = tap / KS, dw = tap % KS;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        half8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          ah[i] = wf[(tap + PP) & 1][i][k][0];
+          al[i] = wf[(tap + PP) & 1][i][k][1];
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+          bh[j] = *reinterpret_cast<const half8*>(&Xh[P][hp][16 * k + 8 * hsel]);
+          bl[j] = *reinterpret_cast<const half8*>(&Xl[P][hp][16 * k + 8 * hsel]);
+        }
+        mma3<TM, TN>(acc, ah, al, bh, bl);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();               // buffer P free; buffer P ^ 1 complete and visible
+  };
+  int q = 0;
+  for (; q + 1 < n; q += 2) {
+    chunk(std::integral_constant<int, 0>(), q);
+    chunk(std::integral_constant<int, 1>(), q + 1);
+  }
+  if (q < n) chunk(std::integral_constant<int, 0>(), q);
+  flag_overflow(a, ovf);
+  conv_epilogue<TM, TN, false>(a, acc, exp2i(sx == kNoExp || RM != 2 ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1);
+}
+
 template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1, int STR = 1>
 void launch_tile(const HaloArgs& a, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit * (a.up == 2 ? 8 : 1);
+  if constexpr (WREG && !D3 && KG == 1 && STR == 1 && KS != 2) {
+    if (a.pipe) {                                  // cfg 32 + c: the pipelined-staging variant
+      hipLaunchKernelGGL((conv_halo_pipe_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);
+      return;
+    }
+  }
   if constexpr (WREG)
     hipLaunchKernelGGL((conv_halo_wreg_kernel<KS, BM, TR, WM, D3, KG, STR>), dim3(grid), dim3(256 * KG), 0, s, a);
   else hipLaunchKernelGGL((conv_halo_x3_kernel<KS, BM, TR, WM, D3>), dim3(grid), dim3(256), 0, s, a);

@@ -161,6 +161,26 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     d3 = true;
     if (cfg >= 24) cfg = 4;
   }
+  if (cfg == 30) {                                 // depth-blocked (17, 1, 1) tile (conv_depth.hip)
+    FSMI_CHECK_ARG(d3 && KS == 1 && KD == 17 && a.str == 1 && !a.up, "%s: tile 30 takes (17, 1, 1) stride-1 "
+                   "volume convs", what);
+    a.nsplit = 1;
+    a.kpc = KD * a.CinP / HKC;
+    a.ws = nullptr;
+    a.ts = nullptr;
+    a.ovf = range_flag_device();
+    const int rc = halo::launch_depth(a, s);
+    if (rc != FSMI_OK) return rc;
+    return finish_launch(what);
+  }
+  // cfg 32 + c: register-weight tile c (2..9) of a 2D map with the pipelined staging (conv_halo.h,
+  // conv_halo_pipe_kernel); the volume instantiation (safe range mode) keeps the plain tile
+  if (cfg >= 32) {
+    cfg -= 32;
+    FSMI_CHECK_ARG(cfg >= 2 && cfg <= 9 && a.str == 1 && !a.up, "%s: pipelined tile 32 + %d (2..9, stride 1)", what,
+                   cfg);
+    a.pipe = d3 ? 0 : 1;
+  }
   const bool pw = cfg >= 24;
   if (pw) {                                        // pointwise LDS-DMA tiles (conv_pw.hip)
     FSMI_CHECK_ARG(cfg <= 26 && KS == 1 && !d3 && HW % 4 == 0, "%s: pointwise tile %d needs a 2D 1x1 conv with "
@@ -312,6 +332,13 @@ extern "C" int fsmi_conv3d_halo_x3_ex(const float* x, int Cin, const void* whi, 
   a.res = res;
   a.res_pre = res_pre;
   a.res_bstride = static_cast<long long>(Cout) * D * H * W;
+  // (17, 1, 1) disparity-axis convs (Conv3dNormActReduced.conv2) on the depth-blocked tile unless a
+  // tile is forced; FSMI_DEPTH_TILE=0 keeps the generic volume tiles (A/B)
+  static const bool depth_tile = [] {
+    const char* e = std::getenv("FSMI_DEPTH_TILE");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (stride == 1 && KS == 1 && KD == 17 && cfg < 0 && depth_tile) cfg = 30;
   const float* seg[1] = {x};
   const int ch[1] = {Cin}, tot[1] = {Cin};
   return run_halo(a, "fsmi_conv3d_halo_x3", seg, ch, tot, 1, whi, wlo, scale_bias, out, Cout, 0, B, Cout, KS, H, W,

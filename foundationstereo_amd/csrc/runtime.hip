@@ -100,6 +100,18 @@ int g_range_safe = 0;
 
 int range_safe() { return __atomic_load_n(&g_range_safe, __ATOMIC_RELAXED); }
 
+// NaN-fill `out` when the range flag is set (one flag read per block): the last node of a captured
+// forward, so a replay that overflowed never returns a finite disparity (fsmi_range_poison)
+__global__ __launch_bounds__(256) void range_poison_kernel(const int* flag, float* out, long long n) {
+  __shared__ int f;
+  if (threadIdx.x == 0) f = *reinterpret_cast<const volatile int*>(flag);
+  __syncthreads();
+  if (!f) return;
+  for (long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * 256)
+    out[i] = __builtin_nanf("");
+}
+
 int* range_flag_device() {
   std::lock_guard<std::mutex> lk(g_range_mu);
   if (!g_range_dev) {
@@ -223,6 +235,17 @@ int fsmi_range_status(int reset, int* overflowed) {
   *overflowed = __atomic_load_n(fsmi::g_range_host, __ATOMIC_ACQUIRE);
   if (reset) __atomic_store_n(fsmi::g_range_host, 0, __ATOMIC_RELEASE);
   return FSMI_OK;
+}
+
+int fsmi_range_poison(float* out, long long n, void* stream) {
+  FSMI_CHECK_ARG(out && n >= 0, "fsmi_range_poison: bad output");
+  int* flag = fsmi::range_flag_device();
+  FSMI_CHECK_ARG(flag, "fsmi_range_poison: host-mapped flag unavailable");
+  if (n == 0) return FSMI_OK;
+  hipStream_t s = fsmi::as_stream(stream);
+  hipLaunchKernelGGL(fsmi::range_poison_kernel, dim3(static_cast<unsigned>((n + 255) / 256 < 64 ? (n + 255) / 256 : 64)), dim3(256),
+                     0, s, flag, out, n);
+  return fsmi::finish_launch("fsmi_range_poison");
 }
 
 int fsmi_set_range_safe(int safe) {

@@ -97,6 +97,9 @@ class ShardedStereo:
         self._local = None          # this rank's shard, (b, 2, 3, H, W), fixed storage
         self._graph = None          # (hipGraph, static output) after capture()
         self._dtype_checked = False
+        # after each replay: synchronise, read the range flag, recover in safe mode (True); or leave
+        # it to the graph's NaN fill and the caller's ops.check_range(), with no host sync (False)
+        self.recover = True
 
     def _local_buffer(self, batch):
         b = batch.shape[0] // self.world
@@ -149,8 +152,8 @@ class ShardedStereo:
         if self._graph is None:
             return self.fn(local[:, 0], local[:, 1])      # an eager FoundationStereo guards itself
         self._graph[0].replay()
-        if not (local.is_cuda and _fs.RANGE_GUARD):
-            return self._graph[1]
+        if not (local.is_cuda and _fs.RANGE_GUARD and self.recover):
+            return self._graph[1]        # the graph NaN-fills its output on overflow (range_poison_)
         # range guard once per replay (one synchronisation): a replay whose flag came back set is
         # recomputed eagerly in safe range mode, and the graph re-captured in that mode
         if not ops.range_overflowed(reset=True):

@@ -288,12 +288,21 @@ class FoundationStereo(nn.Module):
         """core/foundation_stereo.py:194-254.  On a HIP device outside graph capture the range guard
         of the split-precision convs is enforced here, once per forward: the flag is read after the
         forward (one synchronisation) and a forward that overflowed is re-run in safe range mode
-        (ops.guarded) -- no disparity computed past the flag is returned."""
+        (ops.guarded) -- no disparity computed past the flag is returned.  A captured forward ends
+        with a device-side check instead (ops.range_poison_: NaN on overflow)."""
         def run():
             return self._forward(image1, image2, iters, flow_init, test_mode, low_memory, init_disp)
-        if image1.is_cuda and RANGE_GUARD and not torch.cuda.is_current_stream_capturing():
-            return ops.guarded(run)
-        return run()
+        if not (image1.is_cuda and RANGE_GUARD):
+            return run()
+        if torch.cuda.is_current_stream_capturing():
+            # a captured forward cannot synchronise: its last node NaN-fills the disparity when the
+            # flag is set, so a replay that overflowed never returns a finite result (ShardedStereo
+            # reads the flag after a replay and recovers)
+            out = run()
+            if isinstance(out, torch.Tensor) and out.is_contiguous():
+                ops.range_poison_(out)
+            return out
+        return ops.guarded(run)
 
     def _forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):
         B = len(image1)

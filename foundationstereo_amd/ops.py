@@ -401,6 +401,8 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
     stream = _stream(x)
     ws = _split_workspace(x.device, stream, 8 * B * pk.cout * Do * Ho * Wo)
     cfg, nsplit = _tuned(pk.k if stride == 1 else f"{pk.k}s2", pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
+    if cfg == 30 and not _DEPTH_TILE:
+        cfg, nsplit = -1, -1           # A/B: the generic volume tiles (the C side picks)
     _lib.check(_lib.load().fsmi_conv3d_halo_x3_ex(
         _p(x), Cin, _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
         _p(res) if res is not None else None, _p(fatt) if fatt is not None else None, _p(out), B, pk.cout,
@@ -607,6 +609,9 @@ _SPLIT_MAXPIX = int(os.environ.get("FSMI_SPLIT_MAXPIX", "0"))
 # a deep split was chosen to fill, and the extra partial-sum traffic remains.  Measured end to end
 # (cfg2, two runs each): cap 2 +1.3 %, cap 3 -1.2 %, cap 1 -12 %; cfg3 (4 pairs / GPU) neutral.
 _SPLIT_CAP = int(os.environ.get("FSMI_SPLIT_CAP", "2"))
+# (17, 1, 1) volume convs (Conv3dNormActReduced.conv2) on the depth-blocked tile (cfg 30); 0: the
+# generic volume tiles from the tuning table (A/B)
+_DEPTH_TILE = os.environ.get("FSMI_DEPTH_TILE", "1") != "0"
 
 
 _SPLIT_WS = {}
@@ -808,6 +813,14 @@ def check_range():
     if range_overflowed(reset=True):
         raise RangeError("split-precision conv: an activation exceeded fp16's range after the block "
                          "exponent (inputs spanning > 2^9 within one conv tile)")
+
+
+def range_poison_(out: Tensor) -> Tensor:
+    """NaN-fill ``out`` on its stream if the range flag is set (device-side; capturable)."""
+    _check("range_poison", out)
+    assert out.is_contiguous()
+    _lib.check(_lib.load().fsmi_range_poison(_p(out), out.numel(), _stream(out)), "range_poison")
+    return out
 
 
 def reset_range_flag():

@@ -331,6 +331,10 @@ int fsmi_range_status(int reset, int* overflowed);
  * range flag came back set (the reference has no such mode: its convs are fp32 / fp16 autocast,
  * core/update.py:83-159).  Sticky until cleared. */
 int fsmi_set_range_safe(int safe);
+/* Fill out[0..n) with NaN on `stream` when the range flag is set (a device-side check, no host
+ * synchronisation): FoundationStereo.forward appends it to a CAPTURED forward, so a graph replay
+ * whose convs overflowed returns NaN, never a silently wrong disparity. */
+int fsmi_range_poison(float* out, long long n, void* stream);
 int fsmi_get_range_safe(int* safe);
 
 int fsmi_timer_enable(int on);

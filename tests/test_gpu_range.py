@@ -10,7 +10,7 @@ These tests check that no path returns a result computed past the flag:
   precision and leaves the flag clear, on every tile family incl. the pointwise tiles;
 * an all-zero first chunk no longer fixes scale 1 (small later values kept at ~22 bits);
 * ``FoundationStereo.forward`` with an activation layout that overflows mode 2 (a function-
-  preserving 2^-12 / 2^12 rescale of gru04.conv0's first input segment): the forward notices the
+  preserving 2^-14 / 2^14 rescale of gru04.conv0's first input segment): the forward notices the
   flag, re-runs in safe mode and matches the CPU oracle of the unscaled model (< 1e-3 px);
 * the same through ``ShardedStereo``'s captured hipGraph (replay -> flag -> eager safe re-run ->
   re-capture), at world size 1.
@@ -90,14 +90,16 @@ def test_zero_first_chunk(lib, cfg):
 
 
 H, W, MD, ITERS, L, SHIFT = 64, 96, 32, 4, 2, 2
-SCALE = 2.0 ** 12
+SCALE = 2.0 ** 14
 
 
 def _overflowing_model(args):
     """The tiny smoke model with gru04.conv0's first input segment (inp[0], 128 channels) scaled by
-    2^-12 and the matching weight columns by 2^12: the same function (exact powers of two), but
-    the conv's first chunk is now ~2^12 below the motion features that follow it -- beyond mode
-    2's 2^9 headroom."""
+    2^-14 and the matching weight columns by 2^14: the same function (exact powers of two), but
+    the conv's first chunk is now ~2^14 below the motion features that follow it -- beyond mode
+    2's 2^9 headroom.  (2^14 keeps the conv's packed weight rows inside the split's range: a row is
+    scaled by one exponent per output channel, and columns 2^20 apart would push the small ones'
+    lo halves below fp16's normal range -- a weight span no checkpoint has.)"""
     from foundationstereo_amd.foundation_stereo import FoundationStereo
     m = FoundationStereo(args).eval()
     synth.init_module_(m, seed=1234)
@@ -121,7 +123,14 @@ def _overflowing_model(args):
     return m, g(left), g(right), ref
 
 
-def test_forward_recovers_from_overflow(lib):
+@pytest.fixture
+def no_split(monkeypatch):
+    # split-K can put inp[0]'s chunks and the motion chunks in different blocks (each split takes
+    # its own first-chunk exponent); one split per conv makes the overflow certain
+    monkeypatch.setattr(ops, "_SPLIT_MAXPIX", 10 ** 9)
+
+
+def test_forward_recovers_from_overflow(lib, no_split):
     args = synth.make_args(max_disp=MD, corr_levels=L, vit_size="vits")
     m, left, right, ref = _overflowing_model(args)
     n0 = ops.RANGE_RECOVERIES[0]
@@ -146,7 +155,7 @@ def test_forward_recovers_from_overflow(lib):
         fs.RANGE_GUARD = True
 
 
-def test_sharded_replay_recovers_from_overflow(lib):
+def test_sharded_replay_recovers_from_overflow(lib, no_split):
     from foundationstereo_amd.dist import ShardedStereo
     args = synth.make_args(max_disp=MD, corr_levels=L, vit_size="vits")
     m, left, right, ref = _overflowing_model(args)
@@ -172,3 +181,26 @@ def test_sharded_replay_recovers_from_overflow(lib):
     for out in (out1, out2):
         d = float((out.cpu() - ref).abs().max())
         assert d < 1e-3, d
+
+
+def test_captured_forward_poisons_on_overflow(lib, no_split):
+    """Without the per-replay host check (ShardedStereo.recover = False: no synchronisation), a
+    replay whose convs overflowed returns NaN -- the captured forward's last node fills it -- and
+    leaves the flag set for ops.check_range()."""
+    from foundationstereo_amd.dist import ShardedStereo
+    args = synth.make_args(max_disp=MD, corr_levels=L, vit_size="vits")
+    m, left, right, _ = _overflowing_model(args)
+    sh = ShardedStereo(lambda a, b: m(a, b, iters=ITERS, test_mode=True), 0, 1)
+    sh.recover = False
+    batch = torch.stack([left, right], 1)
+    with torch.no_grad():
+        sh.step(batch, (1, H, W))                 # eager warm-up (guarded: recovers, safe mode on)
+        ops.set_range_safe(False)                 # capture the overflowing mode-2 graph
+        ops.range_overflowed(reset=True)
+        sh.capture(batch)
+        ops.range_overflowed(reset=True)
+        out = sh.step(batch, (1, H, W)).clone()
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(out).all())
+    with pytest.raises(ops.RangeError):
+        ops.check_range()

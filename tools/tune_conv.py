@@ -6,8 +6,10 @@ caller leaves cfg / nsplit on auto).  Run on the GPU box:
     python tools/tune_conv.py [--config cfg2 cfg3 ...] [--reps 5] [--only-cfgs 19 20 21 23]
 
 Candidates per shape: the plain tiles (0-9 as they apply), the K-group variants (16 + 3/4/5/7:
-two wave groups per block on alternate chunks, summed in LDS) and for 2D 1x1 layers the pointwise
-LDS-DMA tiles (24-26, conv_pw.hip), each with split-K factors.  With
+two wave groups per block on alternate chunks, summed in LDS), for 2D 1x1 layers the pointwise
+LDS-DMA tiles (24-26, conv_pw.hip), for 2D maps the pipelined-staging register tiles (32 + 2..9)
+and for (17, 1, 1) volume convs the depth-blocked tile (30, conv_depth.hip), each with split-K
+factors.  With
 --only-cfgs only those are timed against the shape's current table entry, the better one kept.
 Shapes of other workloads already in the table are kept as they are.
 """
@@ -34,6 +36,8 @@ ap.add_argument("--only-cfgs", type=int, nargs="*", default=None,
 ap.add_argument("--max-split", type=int, default=8, help="largest split-K factor to time")
 ap.add_argument("--match", default="", help="only re-tune shape keys matching this regex (e.g. '_d(?!1_)' volumes)")
 ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
+ap.add_argument("--base", default=os.path.join(REPO, "tuning", "fsmi_conv.json"),
+                help="table to start from (merged into --out)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 
@@ -92,8 +96,8 @@ def timeit(fn):
 
 
 table = {}
-if os.path.exists(a.out):
-    with open(a.out) as f:
+if os.path.exists(a.base):
+    with open(a.base) as f:
         table = json.load(f)
 entries = dict(table.get("entries", {}))
 prev = dict(entries)
@@ -104,6 +108,8 @@ print(f"[tune] {len(keys)} conv shapes for {a.config}", file=sys.stderr)
 t_start = time.time()
 with torch.no_grad():
     for key in keys:
+        if "s2" in key:                              # stride-2 tiles: their own table entries (s2_bench)
+            continue
         ks, kd, cin, cout, B, D, Hh, Ww = (int(v) for v in re.findall(r"\d+", key))
         if kd == 1 and D == 1:
             x = torch.randn(B, cin, Hh, Ww, device=dev)
@@ -124,6 +130,10 @@ with torch.no_grad():
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
                 + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
                 + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
+        if x.dim() == 4:                            # pipelined-staging variants of the register tiles
+            cfgs += [32 + c for c in cfgs if 2 <= c <= 9]
+        if x.dim() == 5 and ks == 1 and kd == 17:   # depth-blocked (17, 1, 1) tile (no split-K)
+            cfgs.append(30)
         splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck) and s <= a.max_split]
         auto = timeit(lambda: run(-1, -1))
         best = (auto, -1, -1)
@@ -134,7 +144,9 @@ with torch.no_grad():
                 best = (timeit(lambda: run(old["cfg"], old["nsplit"])), old["cfg"], old["nsplit"])
         for c in cfgs:
             for s in splits:
-                if c >= 16 and 2 * s > nck:         # K groups need >= 2 chunks per block
+                if 16 <= c < 24 and 2 * s > nck:   # K groups need >= 2 chunks per block
+                    continue
+                if c == 30 and s > 1:
                     continue
                 t = timeit(lambda: run(c, s))
                 if t < best[0]:
