@@ -62,6 +62,8 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
   const int m0 = (rest / a.B) * 32;
   const int d0 = dt * DB, r0 = rt * TR, c0 = ct * 32;
   const int nck = a.CinP / HKC;
+  __shared__ EpiCoef<32> ecoef;                    // visible to the epilogue after the plane barriers
+  ecoef.fill(a, m0, tid, 256);
 
   HS hs, hs2;
   hs.init(a, tid, r0, c0);
@@ -186,17 +188,23 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
   if (hh >= a.H || ww >= a.W) return;
   const long long P = static_cast<long long>(a.H) * a.W;
   const int hw2 = hh * a.W + ww;
+  const int cb = m0 + 4 * hsel;
+  auto epi = [&](auto act_c) FSMI_HALO_INL {
+    constexpr int ACT = decltype(act_c)::value;
 #pragma unroll
-  for (int j = 0; j < JW; ++j) {
-    const int d = jbase + j;
-    if (d >= a.D) break;
-    const long long hw = static_cast<long long>(d) * P + hw2;
-    const int cb = m0 + 4 * hsel;
-    switch (a.act) {
-      case 1: store_frag<1, true>(a, acc[j], xinv, cb, b, hw, hw2, a.out, a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh); break;
-      case 6: store_frag<6, true>(a, acc[j], xinv, cb, b, hw, hw2, a.out, a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh); break;
-      default: store_frag<0, true>(a, acc[j], xinv, cb, b, hw, hw2, a.out, a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh); break;
+    for (int j = 0; j < JW; ++j) {
+      const int d = jbase + j;
+      if (d >= a.D) break;
+      const long long hw = static_cast<long long>(d) * P + hw2;
+      FragCoef cf;                 // per-cout coefficients from LDS (conv_halo.h EpiCoef)
+      frag_coef_lds<ACT>(xinv, 4 * hsel, ecoef.sb, ecoef.g, cf);
+      store_frag_c<ACT, true>(a, acc[j], cf, cb, b, hw, hw2, a.out, a.res, a.gh, a.gz, a.gatt, a.grh);
     }
+  };
+  switch (a.act) {
+    case 1: epi(std::integral_constant<int, 1>()); break;
+    case 6: epi(std::integral_constant<int, 6>()); break;
+    default: epi(std::integral_constant<int, 0>()); break;
   }
 }
 

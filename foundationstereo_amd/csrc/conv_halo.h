@@ -226,32 +226,49 @@ __device__ __forceinline__ void store_out(const HaloArgs& a, float v, int co, in
   store_el<RESPRE>(a, v, co, b, hw, a.out, a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh);
 }
 
-// One 16-element accumulator fragment (couts cb + (r&3) + 8(r>>2)) at one pixel, activation ACT
-// fixed at compile time and one restrict scope: the fragment's bias / gamma / residual / gate
-// loads are issued together, then 16 branch-free finishes and stores.  (The generic store_el per
-// element compiled to ~400 instructions per fragment with a wait per element: 20-56 % of a
-// block's lifetime went to the epilogue on the nsplit = 1 layers, tools/conv_phases.py.)
-template <int ACT, bool RESPRE>
-__device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, float xinv, int cb, int b,
-                                           long long hw, int hw2, float* __restrict__ out, const float2* __restrict__ sb,
-                                           const float* __restrict__ gamma, const float* __restrict__ res,
-                                           const float* __restrict__ gh, float* __restrict__ gz,
-                                           const float* __restrict__ gatt, float* __restrict__ grh) {
-  const long long HW = a.cstride;
-  const long long OHW = RESPRE && a.up ? a.ocstride : HW;   // output channel stride (transposed conv)
-  float2 q[16];                    // (weight scale 2^-wexp[co], bias[co]) of the 16 rows
+// Per-cout epilogue coefficients of one 16-row fragment (couts cb + (r&3) + 8(r>>2)): the
+// (2^-wexp * xinv, bias) pair and gamma.  Loaded once per cout block of a tile: fetched per
+// fragment they were a dependent L2/HBM round trip before each fragment's 16 stores -- 21-24 us of
+// a 170-200 us block on the nsplit = 1 loop layers (tools/conv_phases.py, round 3).
+struct FragCoef {
+  float2 q[16];
+  float g[16];
+};
+
+template <int ACT>
+__device__ __forceinline__ void frag_coef(const HaloArgs& a, float xinv, int cb, const float2* __restrict__ sb,
+                                          const float* __restrict__ gamma, FragCoef& c) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    q[r] = sb[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)];
-    q[r].x *= xinv;
+    c.q[r] = sb[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)];
+    c.q[r].x *= xinv;
   }
+  if constexpr (!(ACT >= 3 && ACT <= 5)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) c.g[r] = gamma ? gamma[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)] : 1.f;
+  }
+}
+
+// One 16-element accumulator fragment (couts cb + (r&3) + 8(r>>2)) at one pixel, activation ACT
+// fixed at compile time and one restrict scope: the fragment's residual / gate loads are issued
+// together, then 16 branch-free finishes and stores.  (The generic store_el per element compiled to
+// ~400 instructions per fragment with a wait per element: 20-56 % of a block's lifetime went to the
+// epilogue on the nsplit = 1 layers, tools/conv_phases.py.)
+template <int ACT, bool RESPRE>
+__device__ __forceinline__ void store_frag_c(const HaloArgs& a, const f32x16& v, const FragCoef& c, int cb, int b,
+                                             long long hw, int hw2, float* __restrict__ out,
+                                             const float* __restrict__ res, const float* __restrict__ gh,
+                                             float* __restrict__ gz, const float* __restrict__ gatt,
+                                             float* __restrict__ grh) {
+  const long long HW = a.cstride;
+  const long long OHW = RESPRE && a.up ? a.ocstride : HW;   // output channel stride (transposed conv)
   if constexpr (ACT >= 3 && ACT <= 5) {
     const float at = ACT == 3 ? 0.f : gatt[static_cast<size_t>(b) * HW + hw];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = cb + (r & 3) + 8 * (r >> 2);
       if (co >= a.Cout) continue;
-      const float x = v[r] * q[r].x + q[r].y;
+      const float x = v[r] * c.q[r].x + c.q[r].y;
       const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
       if constexpr (ACT == 3) {
         const float sg = sigm_h(x);
@@ -267,9 +284,6 @@ __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, f
     }
     return;
   } else {
-    float gv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) gv[r] = gamma ? gamma[min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1)] : 1.f;
     const bool pre = RESPRE && a.res_pre;
     // FeatureAtt gate (volumes only): sigmoid(fatt[b, co, hw2]), hw2 = h * W + w of the output plane
     const float* __restrict__ fatt = RESPRE ? a.fatt : nullptr;
@@ -278,17 +292,28 @@ __device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, f
     for (int r = 0; r < 16; ++r) {
       const int co = cb + (r & 3) + 8 * (r >> 2);
       if (co >= a.Cout) continue;
-      float x = v[r] * q[r].x + q[r].y;
+      float x = v[r] * c.q[r].x + c.q[r].y;
       const float rv = res ? res[b * a.res_bstride + static_cast<long long>(co) * HW + hw] : 0.f;
       if (pre) x += rv;            // ResNet tail: act(conv + bias + res)
       if constexpr (ACT == 1) x = fmaxf(x, 0.f);
       else if constexpr (ACT == 2) x = gelu_erf_h(x);
       else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
-      if (!pre) x = x * a.alpha * gv[r] + rv;
+      if (!pre) x = x * a.alpha * c.g[r] + rv;
       if (fatt) x *= sigm_h(fatt[(static_cast<long long>(b) * a.Cout + co) * P + hw2]);
       out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * OHW + hw] = x;
     }
   }
+}
+
+template <int ACT, bool RESPRE>
+__device__ __forceinline__ void store_frag(const HaloArgs& a, const f32x16& v, float xinv, int cb, int b,
+                                           long long hw, int hw2, float* __restrict__ out, const float2* __restrict__ sb,
+                                           const float* __restrict__ gamma, const float* __restrict__ res,
+                                           const float* __restrict__ gh, float* __restrict__ gz,
+                                           const float* __restrict__ gatt, float* __restrict__ grh) {
+  FragCoef c;
+  frag_coef<ACT>(a, xinv, cb, sb, gamma, c);
+  store_frag_c<ACT, RESPRE>(a, v, c, cb, b, hw, hw2, out, res, gh, gz, gatt, grh);
 }
 
 // 4 consecutive pixels of one channel, one restrict scope
@@ -540,10 +565,42 @@ __device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM
     }
 }
 
+// The block's per-cout epilogue coefficients, staged into LDS at the start of the kernel (their
+// global loads hidden under the main loop): lsb[c] = (2^-wexp, bias) and lg[c] = gamma of cout
+// m0 + c (clamped to Cout - 1).  Fetched from global memory per fragment in the epilogue they were a
+// dependent L2/HBM round trip before each fragment's 16 stores -- 21-24 us of a 170-200 us block on
+// the nsplit = 1 loop layers (tools/conv_phases.py, round 3); from LDS each is ~100 cycles, and one
+// fragment's coefficients at a time keep the register peak of the per-fragment loads.
+template <int BM>
+struct EpiCoef {
+  float2 sb[BM];
+  float g[BM];
+  __device__ __forceinline__ void fill(const HaloArgs& a, int m0, int tid, int nthreads) {
+    for (int e = tid; e < BM; e += nthreads) {
+      const int co = min(m0 + e, a.Cout - 1);
+      sb[e] = a.sb[co];
+      g[e] = a.gamma ? a.gamma[co] : 1.f;
+    }
+  }
+};
+
+template <int ACT>
+__device__ __forceinline__ void frag_coef_lds(float xinv, int cl, const float2* lsb, const float* lg, FragCoef& c) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    c.q[r] = lsb[cl + (r & 3) + 8 * (r >> 2)];
+    c.q[r].x *= xinv;
+  }
+  if constexpr (!(ACT >= 3 && ACT <= 5)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) c.g[r] = lg[cl + (r & 3) + 8 * (r >> 2)];
+  }
+}
+
 // Non-split epilogue of the block's tile with the activation fixed at compile time
 template <int ACT, int TM, int TN, bool D3>
 __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv, const TileCoord& t,
-                                         int wm, int wn, int lane, unsigned fown) {
+                                         int wm, int wn, int lane, unsigned fown, const float2* lsb, const float* lg) {
   const int hsel = lane >> 5, rl = lane & 31;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -554,9 +611,13 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
                                     : static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
-      if ((fown >> (i * TN + j)) & 1u)
-      store_frag<ACT, D3>(a, acc[i][j], xinv, t.m0 + (wm * TM + i) * 32 + 4 * hsel, t.b, hw, hh * a.W + ww, a.out,
-                          a.sb, a.gamma, a.res, a.gh, a.gz, a.gatt, a.grh);
+      if ((fown >> (i * TN + j)) & 1u) {
+        const int cl = (wm * TM + i) * 32 + 4 * hsel;
+        FragCoef c;
+        frag_coef_lds<ACT>(xinv, cl, lsb, lg, c);
+        store_frag_c<ACT, D3>(a, acc[i][j], c, t.m0 + cl, t.b, hw, hh * a.W + ww, a.out, a.res, a.gh, a.gz, a.gatt,
+                              a.grh);
+      }
   }
 }
 
@@ -564,7 +625,7 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
 template <int TM, int TN, bool D3>
 __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv,
                                               const TileCoord& t, int wm, int wn, int lane, bool partial,
-                                              unsigned fown = ~0u) {
+                                              const float2* lsb, const float* lg, unsigned fown = ~0u) {
   const int hsel = lane >> 5, rl = lane & 31;
   const long long HW = a.cstride;
   if (partial) {                   // raw partial sums into ws slot t.split; a reduce applies the epilogue
@@ -587,13 +648,13 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
     return;
   }
   switch (a.act) {                 // uniform: one specialised tile epilogue per activation
-    case 1: epi_tile<1, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
-    case 2: epi_tile<2, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
-    case 3: epi_tile<3, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
-    case 4: epi_tile<4, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
-    case 5: epi_tile<5, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
-    case 6: epi_tile<6, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
-    default: epi_tile<0, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown); break;
+    case 1: epi_tile<1, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 2: epi_tile<2, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 3: epi_tile<3, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 4: epi_tile<4, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 5: epi_tile<5, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 6: epi_tile<6, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    default: epi_tile<0, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
   }
 }
 
@@ -623,6 +684,8 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
   const int m0 = tc.m0;
   const int nck = a.CinP / HKC;
   const int nq = D3 ? a.KD * nck : nck;            // chunks = (kd, 32-channel chunk) pairs, kd major
+  __shared__ EpiCoef<BM> ecoef;                    // visible to the epilogue after the main loop's barriers
+  if (a.nsplit == 1) ecoef.fill(a, m0, tid, 256);
 
   const bool w_full = m0 + BM <= a.CoutP;          // block-uniform: only the last cout tile is ragged
   uint4 rwh[W_PER_T], rwl[W_PER_T];
@@ -761,7 +824,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
     }
   }
   flag_overflow(a, ovf);
-  conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1);
+  conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1, ecoef.sb, ecoef.g);
 }
 
 // ---------------------------------------------------------------- cfg 2/3: weights in registers
@@ -788,6 +851,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   // K-group exchange (2 x 16 KB): the halo buffers when they are large enough, else its own
   constexpr bool XCH_IN_HALO = sizeof(_Float16) * KG * HS::NHP * HROW >= 16 * 256 * sizeof(float);
   __shared__ __attribute__((aligned(16))) float xch_own[(KG == 2 && !XCH_IN_HALO) ? 2 * 16 * 256 : 1];
+  __shared__ EpiCoef<BM> ecoef;
 
   const int grp = KG == 1 ? 0 : static_cast<int>(threadIdx.x >> 8);
   const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
@@ -968,7 +1032,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
       }
       xinv = 1.f;
     }
-    conv_epilogue<TM, TN, D3>(a, acc, xinv, tc, wm, wn, lane, partial, fown);
+    conv_epilogue<TM, TN, D3>(a, acc, xinv, tc, wm, wn, lane, partial, ecoef.sb, ecoef.g, fown);
     if (tsb && threadIdx.x == 0) {
       tsb[38] = wall_clock64();
       tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
@@ -997,6 +1061,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
   }
   const TileCoord tc = decode_tile<BM, TR, D3>(a, bid, nb);
   const int c0 = tc.split * a.kpc;
+  if (a.nsplit == 1) ecoef.fill(a, tc.m0, threadIdx.x, 256 * KG);   // read after the main loop's barriers
   segment(tc, c0, min(nq, c0 + a.kpc), a.nsplit > 1);
 }
 
@@ -1031,6 +1096,8 @@ __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
   const int hsel = lane >> 5, rl = lane & 31;
   const int nck = a.CinP / HKC;
   const TileCoord tc = decode_tile<BM, TR, false>(a, blockIdx.x, gridDim.x);
+  __shared__ EpiCoef<BM> ecoef;                    // visible to the epilogue after the main loop's barriers
+  if (a.nsplit == 1) ecoef.fill(a, tc.m0, tid, 256);
   const int c_first = tc.split * a.kpc;
   const int c_end = min(nck, c_first + a.kpc);
   const int n = c_end - c_first;                   // >= 1: no empty splits (run_halo)
@@ -1127,7 +1194,8 @@ __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
   }
   if (q < n) chunk(std::integral_constant<int, 0>(), q);
   flag_overflow(a, ovf);
-  conv_epilogue<TM, TN, false>(a, acc, exp2i(sx == kNoExp || RM != 2 ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1);
+  conv_epilogue<TM, TN, false>(a, acc, exp2i(sx == kNoExp || RM != 2 ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1,
+                                ecoef.sb, ecoef.g);
 }
 
 template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1, int STR = 1>

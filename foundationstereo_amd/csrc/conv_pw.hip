@@ -18,6 +18,10 @@
 // Entry: run_halo (conv_halo_x3.hip) with cfg 24-26; KS = 1, 2D, H*W % 4 == 0, 16-B aligned segments.
 #include "conv_halo.h"
 
+#ifndef FSMI_PW_TWOBAR
+#define FSMI_PW_TWOBAR 0                           // 1: the round-2 schedule (a second barrier per chunk)
+#endif
+
 // dma16 writes m0 (the LDS-DMA base): nothing else in these kernels uses it
 #pragma clang diagnostic ignored "-Winline-asm"
 
@@ -69,6 +73,8 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
   const int b = ptile / a.nct;
   const long long px0 = static_cast<long long>(ptile - b * a.nct) * PX;
   const int c_begin = split * a.kpc, c_end = min(nck, c_begin + a.kpc), n = c_end - c_begin;
+  __shared__ EpiCoef<BM> ecoef;                    // visible to the epilogue after the ring's barriers
+  if (a.nsplit == 1) ecoef.fill(a, m0, tid, 256);
 
   // this lane's DMA elements: op o moves flat quad (wave * OPS + o) * 64 + lane of the chunk
   int drow[OPS];
@@ -141,9 +147,18 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
     constexpr int P = decltype(par_c)::value;
     const int c = c_begin + q;
     load_wf(std::integral_constant<int, P ^ 1>(), min(c + 1, c_end - 1));
+#if FSMI_PW_TWOBAR
     dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
     wait_vmcnt<2 * OPS + 4 * TM>();                // this wave's part of chunk q has landed
     bar();                                         // ... and every wave's
+#else
+    // one barrier per chunk: chunk q's DMA is waited for (chunks q+1 .. q+NS-2 and the weights just
+    // issued may stay in flight), the barrier makes every wave's part visible AND retires every
+    // wave's reads of chunk q-1's slot, which chunk q+NS-1 then refills
+    wait_vmcnt<(NS - 2) * OPS + 4 * TM>();
+    bar();
+    dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
+#endif
     const float* xs = ring[q % NS];
     // block exponent (range mode 2) from the first chunk holding a nonzero value (an all-zero first
     // chunk would leave scale 1 and drop small later values to fp16 subnormals)
@@ -190,8 +205,10 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
       }
       mma3<TM, TN>(acc, ah, al, bh, bl);
     }
+#if FSMI_PW_TWOBAR
     wait_lgkm0();
     bar();                                         // every wave is done with slot q % NS
+#endif
   };
   int q = 0;
   for (; q + 1 < n; q += 2) {
@@ -226,9 +243,12 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
       if (!pix_ok[j]) continue;
       const long long hw = px0 + (wn * TN + j) * 32 + rl;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        store_frag<ACT, false>(a, acc[i][j], xinv, m0 + (wm * TM + i) * 32 + 4 * hsel, b, hw, 0, a.out, a.sb, a.gamma,
-                               a.res, a.gh, a.gz, a.gatt, a.grh);
+      for (int i = 0; i < TM; ++i) {
+        const int cl = (wm * TM + i) * 32 + 4 * hsel;
+        FragCoef cf;               // per-cout coefficients from LDS (conv_halo.h EpiCoef)
+        frag_coef_lds<ACT>(xinv, cl, ecoef.sb, ecoef.g, cf);
+        store_frag_c<ACT, false>(a, acc[i][j], cf, m0 + cl, b, hw, 0, a.out, a.res, a.gh, a.gz, a.gatt, a.grh);
+      }
     }
   };
   switch (a.act) {

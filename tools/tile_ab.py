@@ -35,6 +35,7 @@ LOOP = [("gru04.conv0", 384, 384, 3, 120, 160), ("gru04.conv1", 512, 512, 3, 120
         ("enc.convc2", 256, 256, 3, 120, 160), ("enc.conv", 320, 127, 3, 120, 160),
         ("head.conv", 128, 128, 3, 120, 160), ("enc.convd2", 64, 64, 3, 120, 160),
         ("gru04.zr_s", 512, 256, 1, 120, 160), ("gru04.q_s", 512, 128, 1, 120, 160),
+        ("enc.convc1", 1044, 256, 1, 120, 160), ("head.pw1", 128, 512, 1, 120, 160), ("head.pw2", 512, 128, 1, 120, 160),
         ("gru08.conv0", 384, 384, 3, 60, 80), ("gru08.conv1", 512, 512, 3, 60, 80),
         ("gru08.zr_l", 512, 256, 3, 60, 80), ("gru08.q_l", 512, 128, 3, 60, 80),
         ("gru16.conv1", 384, 384, 3, 30, 40), ("gru16.zr_l", 384, 256, 3, 30, 40)]
@@ -82,9 +83,11 @@ if a.set in ("loop", "all"):
         cands = [(tcfg, tns)]
         if 2 <= tcfg <= 9:
             cands.append((tcfg + 32, tns))
-        elif tcfg >= 24 or tcfg >= 16:
+        elif tcfg >= 16:
             for c in (3, 4, 9):
                 cands += [(c, tns), (c + 32, tns)]
+        if k == 1:
+            cands += [(c, ns) for c in (24, 25, 26) for ns in (1, 2, 3) if (c, ns) != (tcfg, tns)]
         fl = 2.0 * cin * cout * k * k * H * W
         for cfg, ns in cands:
             fn = lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=cfg, nsplit=ns)  # noqa: E731
