@@ -260,26 +260,41 @@ __device__ __forceinline__ void store_frag_c(const HaloArgs& a, const f32x16& v,
                                              const float* __restrict__ res, const float* __restrict__ gh,
                                              float* __restrict__ gz, const float* __restrict__ gatt,
                                              float* __restrict__ grh) {
+  // Every load of the fragment is issued before its first store: vmcnt counts loads and stores in
+  // issue order, so a load placed after a store waits for that store's completion too -- with the
+  // loads interleaved per element (and the residual load inside a per-element branch) the compiler
+  // emitted s_waitcnt vmcnt(0) after every store, ~128 serialised store round trips per wave
+  // (20 us of a 185 us block, round 3).  Rows past Cout only exist in the last cout tile.
   const long long HW = a.cstride;
   const long long OHW = RESPRE && a.up ? a.ocstride : HW;   // output channel stride (transposed conv)
+  const bool full = (cb - (cb & 4)) + 32 <= a.Cout;          // all 32 rows of the fragment exist
   if constexpr (ACT >= 3 && ACT <= 5) {
+    float ghv[16], gzv[16], ov[16];
     const float at = ACT == 3 ? 0.f : gatt[static_cast<size_t>(b) * HW + hw];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
+      const int co = min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1);
+      const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
+      ghv[r] = (ACT != 3 || co >= a.gHd) ? gh[g] : 0.f;
+      gzv[r] = ACT != 3 ? gz[g] : 0.f;
+      ov[r] = ACT == 5 ? out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
       const int co = cb + (r & 3) + 8 * (r >> 2);
-      if (co >= a.Cout) continue;
+      if (!full && co >= a.Cout) continue;
       const float x = v[r] * c.q[r].x + c.q[r].y;
       const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
       if constexpr (ACT == 3) {
         const float sg = sigm_h(x);
         if (co < a.gHd) gz[g] = sg;
-        else grh[g] = sg * gh[g];
+        else grh[g] = sg * ghv[r];
       } else {
-        const float z = gz[g];
-        const float hn = (1.f - z) * gh[g] + z * tanhf(x);
+        const float z = gzv[r];
+        const float hn = (1.f - z) * ghv[r] + z * tanhf(x);
         float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
         if constexpr (ACT == 4) *o = hn * at;
-        else *o = *o + hn * (1.f - at);
+        else *o = ov[r] + hn * (1.f - at);
       }
     }
     return;
@@ -288,18 +303,29 @@ __device__ __forceinline__ void store_frag_c(const HaloArgs& a, const f32x16& v,
     // FeatureAtt gate (volumes only): sigmoid(fatt[b, co, hw2]), hw2 = h * W + w of the output plane
     const float* __restrict__ fatt = RESPRE ? a.fatt : nullptr;
     const long long P = static_cast<long long>(a.H) * a.W;
+    float rv[16], fv[16];
+    if (res || fatt) {             // block-uniform; the common case has no loads at all
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = min(cb + (r & 3) + 8 * (r >> 2), a.Cout - 1);
+        rv[r] = res ? res[b * a.res_bstride + static_cast<long long>(co) * HW + hw] : 0.f;
+        fv[r] = fatt ? fatt[(static_cast<long long>(b) * a.Cout + co) * P + hw2] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) rv[r] = fv[r] = 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = cb + (r & 3) + 8 * (r >> 2);
-      if (co >= a.Cout) continue;
+      if (!full && co >= a.Cout) continue;
       float x = v[r] * c.q[r].x + c.q[r].y;
-      const float rv = res ? res[b * a.res_bstride + static_cast<long long>(co) * HW + hw] : 0.f;
-      if (pre) x += rv;            // ResNet tail: act(conv + bias + res)
+      if (pre) x += rv[r];         // ResNet tail: act(conv + bias + res)
       if constexpr (ACT == 1) x = fmaxf(x, 0.f);
       else if constexpr (ACT == 2) x = gelu_erf_h(x);
       else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
-      if (!pre) x = x * a.alpha * c.g[r] + rv;
-      if (fatt) x *= sigm_h(fatt[(static_cast<long long>(b) * a.Cout + co) * P + hw2]);
+      if (!pre) x = x * a.alpha * c.g[r] + rv[r];
+      if (fatt) x *= sigm_h(fv[r]);
       out[b * a.out_bstride + static_cast<long long>(a.co0 + co) * OHW + hw] = x;
     }
   }
@@ -322,8 +348,60 @@ __device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], i
                                        const float* __restrict__ gamma, const float* __restrict__ res,
                                        const float* __restrict__ gh, float* __restrict__ gz,
                                        const float* __restrict__ gatt, float* __restrict__ grh) {
+  // the split-K reduce's epilogue for 4 consecutive pixels: every operand load (gates, residual,
+  // FeatureAtt gate) is issued before the first store -- interleaved, each load waited for the
+  // stores issued ahead of it (vmcnt counts both in order)
+  const long long HW = a.cstride;
+  const float2 q = sb[co];
+  if (a.act >= 3 && a.act <= 5) {
+    const size_t g = (static_cast<size_t>(b) * a.gHd + (co % a.gHd)) * HW + hw;
+    float hv[4], zv[4], ov[4], at[4];
+    float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) store_el<true>(a, v[k], co, b, hw + k, out, sb, gamma, res, gh, gz, gatt, grh);
+    for (int k = 0; k < 4; ++k) {
+      hv[k] = (a.act != 3 || co >= a.gHd) ? gh[g + k] : 0.f;
+      zv[k] = a.act != 3 ? gz[g + k] : 0.f;
+      ov[k] = a.act == 5 ? o[k] : 0.f;
+      at[k] = a.act != 3 ? gatt[static_cast<size_t>(b) * HW + hw + k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = v[k] * q.x + q.y;
+      if (a.act == 3) {
+        const float sg = sigm_h(x);
+        if (co < a.gHd) gz[g + k] = sg;
+        else grh[g + k] = sg * hv[k];
+      } else {
+        const float hn = (1.f - zv[k]) * hv[k] + zv[k] * tanhf(x);
+        o[k] = a.act == 4 ? hn * at[k] : ov[k] + hn * (1.f - at[k]);
+      }
+    }
+    return;
+  }
+  float rv[4], fv[4];
+  const long long P = static_cast<long long>(a.H) * a.W;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rv[k] = res ? res[b * a.res_bstride + static_cast<long long>(co) * HW + hw + k] : 0.f;
+    fv[k] = a.fatt ? a.fatt[(static_cast<long long>(b) * a.Cout + co) * P + (hw + k) % P] : 0.f;
+  }
+  const float gm = gamma ? gamma[co] : 1.f;
+  float* o = out + b * a.out_bstride + static_cast<long long>(a.co0 + co) * HW + hw;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float x = v[k] * q.x + q.y;
+    if (a.res_pre) {             // ResNet tail: act(v + bias + res)
+      x += rv[k];
+      x = a.act == 1 ? fmaxf(x, 0.f) : (a.act == 6 ? (x >= 0.f ? x : 0.01f * x) : x);
+    } else {
+      if (a.act == 1) x = fmaxf(x, 0.f);
+      else if (a.act == 2) x = gelu_erf_h(x);
+      else if (a.act == 6) x = x >= 0.f ? x : 0.01f * x;
+      x = x * a.alpha * gm + rv[k];
+    }
+    if (a.fatt) x *= sigm_h(fv[k]);
+    o[k] = x;
+  }
 }
 
 // ---------------------------------------------------------------- shared pieces
