@@ -513,6 +513,15 @@ struct HaloStage {
   }
 };
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>());
+    static_for<B + 1, E>(f);
+  }
+}
+
 struct TileCoord {
   int m0, b, d0, r0, c0, split;
 };
@@ -1222,15 +1231,30 @@ __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
   if (n > 1) hs.load(a, tc.b, c_first + 1);
   __syncthreads();
 
-  // chunk q on buffer P = q & 1; tap t uses weight buffer (t + PP) & 1 and prefetches tap t + 1
+  // chunk q on buffer P = q & 1; tap t uses weight buffer (t + PP) & 1 and prefetches tap t + 1.
+  // The B fragments (LDS) of each (tap, k half) step are read one step ahead into the other half of
+  // a double buffer, so a step's MFMAs never wait on the LDS latency of their own reads (only the
+  // chunk's first step does: the next chunk's buffer is complete only after the closing barrier)
   auto chunk = [&](auto par_c, int q) FSMI_HALO_INL {
     constexpr int P = decltype(par_c)::value;
     constexpr int PP = (NTAP & 1) ? P : 0;
     const int cc = c_first + q;
+    half8 bh[2][TN], bl[2][TN];    // [step parity][j]
+    auto read_b = [&](auto s_c) FSMI_HALO_INL {    // B fragments of step S = 2 tap + k
+      constexpr int S = decltype(s_c)::value;
+      constexpr int tp = S / 2, k = S % 2, dh = tp / KS, dw = tp % KS;
 #pragma unroll
-    for (int tap = 0; tap < NTAP; ++tap) {
-      const bool last = tap + 1 == NTAP;
-      if (((tap + PP) & 1) == 0) {
+      for (int j = 0; j < TN; ++j) {
+        const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
+        bh[S & 1][j] = *reinterpret_cast<const half8*>(&Xh[P][hp][16 * k + 8 * hsel]);
+        bl[S & 1][j] = *reinterpret_cast<const half8*>(&Xl[P][hp][16 * k + 8 * hsel]);
+      }
+    };
+    read_b(std::integral_constant<int, 0>());
+    static_for<0, NTAP>([&](auto tap_c) FSMI_HALO_INL {
+      constexpr int tap = decltype(tap_c)::value;
+      constexpr bool last = tap + 1 == NTAP;
+      if constexpr (((tap + PP) & 1) == 0) {
         load_wf(std::integral_constant<int, 1>(), last ? min(cc + 1, c_end - 1) : cc, last ? 0 : tap + 1);
       } else {
         load_wf(std::integral_constant<int, 0>(), last ? min(cc + 1, c_end - 1) : cc, last ? 0 : tap + 1);
@@ -1244,25 +1268,19 @@ __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
         if (q + 2 < n) hs.load(a, tc.b, cc + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
-      const int dh = tap / KS, dw = tap % KS;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        half8 ah[TM], al[TM], bh[TN], bl[TN];
+      static_for<0, 2>([&](auto k_c) FSMI_HALO_INL {
+        constexpr int k = decltype(k_c)::value, S = 2 * tap + k;
+        if constexpr (S + 1 < 2 * NTAP) read_b(std::integral_constant<int, S + 1>());   // next step's B
+        half8 ah[TM], al[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           ah[i] = wf[(tap + PP) & 1][i][k][0];
           al[i] = wf[(tap + PP) & 1][i][k][1];
         }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int hp = ((wn * TN + j) + dh) * HS::HC + rl + dw;
-          bh[j] = *reinterpret_cast<const half8*>(&Xh[P][hp][16 * k + 8 * hsel]);
-          bl[j] = *reinterpret_cast<const half8*>(&Xl[P][hp][16 * k + 8 * hsel]);
-        }
-        mma3<TM, TN>(acc, ah, al, bh, bl);
-      }
+        mma3<TM, TN>(acc, ah, al, bh[S & 1], bl[S & 1]);
+      });
       __builtin_amdgcn_sched_barrier(0);
-    }
+    });
     __syncthreads();               // buffer P free; buffer P ^ 1 complete and visible
   };
   int q = 0;
