@@ -56,6 +56,9 @@ constexpr int range_mode() { return FSMI_HALO_RANGE == 1 ? (D3 ? 1 : 2) : FSMI_H
 #else
 #define FSMI_HALO_INL
 #endif
+#ifndef FSMI_WREG_BPREF
+#define FSMI_WREG_BPREF 1                            // 0: A/B build, B fragments read just before their MFMAs
+#endif
 #ifndef FSMI_HALO_PERCOUT
 #define FSMI_HALO_PERCOUT 1                          // 0: A/B build reading one weight scale (row 0's)
 #endif
@@ -989,14 +992,28 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
     const int n_g = c_first < cc_end ? (cc_end - c_first + KG - 1) / KG : 0;
     const int c_last = c_first + KG * max(n_g - 1, 0);
 
-    // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the next
+    // tap t of a chunk uses register buffer (t + P) & 1, P = chunk parity; each tap prefetches the
+    // next.  The B fragments (LDS) of each (tap, k half) step are read one step ahead (as the
+    // pipelined tiles), so a step's MFMAs never wait on their own reads' LDS latency.
     auto chunk = [&](auto par_c, int cc) FSMI_HALO_INL {
       // an even tap count (KS = 2) starts every chunk on buffer 0; an odd one alternates
       constexpr int P = (NTAP & 1) ? decltype(par_c)::value : 0;
+      half8 bh[2][TN], bl[2][TN];  // [step parity][j]
+      auto read_b = [&](auto s_c) FSMI_HALO_INL {  // B fragments of step S = 2 tap + k
+        constexpr int S = decltype(s_c)::value;
+        constexpr int tp = S / 2, k = S % 2, dh = tp / KS, dw = tp % KS;
 #pragma unroll
-      for (int tap = 0; tap < NTAP; ++tap) {
-        const bool last = tap + 1 == NTAP;
-        if (((tap + P) & 1) == 0) {
+        for (int j = 0; j < TN; ++j) {
+          const int hp = ((wn * TN + j) * STR + dh) * HS::HC + STR * rl + dw;
+          bh[S & 1][j] = *reinterpret_cast<const half8*>(&gXh[hp][16 * k + 8 * hsel]);
+          bl[S & 1][j] = *reinterpret_cast<const half8*>(&gXl[hp][16 * k + 8 * hsel]);
+        }
+      };
+      if constexpr (FSMI_WREG_BPREF) read_b(std::integral_constant<int, 0>());
+      static_for<0, NTAP>([&](auto tap_c) FSMI_HALO_INL {
+        constexpr int tap = decltype(tap_c)::value;
+        constexpr bool last = tap + 1 == NTAP;
+        if constexpr (((tap + P) & 1) == 0) {
           load_wf(std::integral_constant<int, 1>(), last ? min(cc + KG, c_last) : cc, last ? 0 : tap + 1);
         } else {
           load_wf(std::integral_constant<int, 0>(), last ? min(cc + KG, c_last) : cc, last ? 0 : tap + 1);
@@ -1005,27 +1022,25 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
         // below the last MFMA and reuses the current buffer's registers -- a single buffer whose
         // L2 round trip every tap then waits on
         __builtin_amdgcn_sched_barrier(0);
-        const int dh = tap / KS, dw = tap % KS;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          half8 ah[TM], al[TM], bh[TN], bl[TN];
+        static_for<0, 2>([&](auto k_c) FSMI_HALO_INL {
+          constexpr int k = decltype(k_c)::value, S = 2 * tap + k;
+          if constexpr (FSMI_WREG_BPREF) {
+            if constexpr (S + 1 < 2 * NTAP) read_b(std::integral_constant<int, S + 1>());   // next step's B
+          } else {
+            read_b(std::integral_constant<int, S>());   // A/B: this step's B, read just before its MFMAs
+          }
+          half8 ah[TM], al[TM];
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
             ah[i] = wf[(tap + P) & 1][i][k][0];
             al[i] = wf[(tap + P) & 1][i][k][1];
           }
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int hp = ((wn * TN + j) * STR + dh) * HS::HC + STR * rl + dw;
-            bh[j] = *reinterpret_cast<const half8*>(&gXh[hp][16 * k + 8 * hsel]);
-            bl[j] = *reinterpret_cast<const half8*>(&gXl[hp][16 * k + 8 * hsel]);
-          }
-          mma3<TM, TN>(acc, ah, al, bh, bl);
-        }
+          mma3<TM, TN>(acc, ah, al, bh[S & 1], bl[S & 1]);
+        });
         // keep the one-tap-ahead structure: without this fence the scheduler hoists every
         // tap's loads of the unrolled chunk to its top (500 registers, 1 wave per SIMD)
         __builtin_amdgcn_sched_barrier(0);
-      }
+      });
     };
     int sx = kNoExp;               // block (group) exponent of the segment (see chunk_exp)
     bool ovf = false;
