@@ -38,6 +38,7 @@ ap.add_argument("--reps", type=int, default=12, help="graph replays per evaluati
 ap.add_argument("--min-gain", type=float, default=0.003, help="relative step gain to keep a change")
 ap.add_argument("--max-split", type=int, default=4, help="largest split-K factor among the alternatives")
 ap.add_argument("--write", action="store_true", help="merge the result into tuning/fsmi_conv.json")
+ap.add_argument("--out", default="", help="also write the merged table here (e.g. under gpurun_out/)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 t_start = time.time()
@@ -132,10 +133,14 @@ def candidates(key):
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
                 + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
                 + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
+        if x.dim() == 4:                            # pipelined-staging variants of the register tiles
+            cfgs += [32 + c for c in cfgs if 2 <= c <= 9]
+        if x.dim() == 5 and ks == 1 and kd == 17:   # depth-blocked (17, 1, 1) tile
+            cfgs.append(30)
         res = []
         for c in cfgs:
             for s in (1, 2, 3, 4):
-                if s > cap or (s > 1 and s > nck) or (c >= 16 and c < 24 and 2 * s > nck):
+                if s > cap or (s > 1 and s > nck) or (c >= 16 and c < 24 and 2 * s > nck) or (c == 30 and s > 1):
                     continue
                 if x.dim() == 4:
                     f = lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=c, nsplit=s)  # noqa: E731
@@ -151,7 +156,8 @@ def table_us(key):
     return e.get("us", 0.0) if e else 0.0
 
 
-order = sorted(counts, key=lambda k: -counts[k] * max(table_us(k), 1.0))[:a.top]
+order = sorted((k for k in counts if "s2" not in k),     # stride-2 tiles keep their s2_bench entries
+               key=lambda k: -counts[k] * max(table_us(k), 1.0))[:a.top]
 print(f"[insitu] {len(counts)} conv shapes, searching {len(order)}", file=sys.stderr, flush=True)
 base = min(evaluate(), evaluate())
 start = base
@@ -189,3 +195,9 @@ if a.write and changes and final < start:
     with open(ops._TUNE_PATH, "w") as f:
         json.dump(db, f, indent=1, sort_keys=True)
     print(f"[insitu] wrote {len(changes)} changes to {ops._TUNE_PATH}", file=sys.stderr)
+if a.out and changes and final < start:
+    with open(ops._TUNE_PATH) as f:
+        db = json.load(f)
+    db["entries"].update(changes)
+    with open(a.out, "w") as f:
+        json.dump(db, f, indent=1, sort_keys=True)
