@@ -39,6 +39,8 @@ ap.add_argument("--min-gain", type=float, default=0.003, help="relative step gai
 ap.add_argument("--max-split", type=int, default=4, help="largest split-K factor among the alternatives")
 ap.add_argument("--write", action="store_true", help="merge the result into tuning/fsmi_conv.json")
 ap.add_argument("--out", default="", help="also write the merged table here (e.g. under gpurun_out/)")
+ap.add_argument("--nosplit", action="store_true", help="also try each shape's current tile without split-K")
+ap.add_argument("--alts-only", action="store_true", help="skip the isolated candidate search (with --nosplit)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 t_start = time.time()
@@ -118,6 +120,8 @@ def graph_time(f, reps=10):
 
 def candidates(key):
     """the a.alts fastest (cfg, nsplit) of a shape timed alone (graph-timed), nsplit <= cap"""
+    if a.alts_only:
+        return [], table_us(key)
     ks, kd, cin, cout, B, D, Hh, Ww = (int(v) for v in re.findall(r"\d+", key))
     with torch.no_grad():
         if kd == 1 and D == 1:
@@ -166,6 +170,8 @@ changes = {}
 for n, key in enumerate(order):
     cur = table.get(key)
     alts, best_alone = candidates(key)
+    if a.nosplit and cur is not None and (cur["cfg"], 1) not in alts and cur["cfg"] != 30:
+        alts = [(cur["cfg"], 1)] + alts          # no split-K: other streams fill the tail in situ
     print(f"[insitu] {n + 1}/{len(order)} {key} x{counts[key]}: alternatives {alts}, step {base:.3f} ms "
           f"({(time.time() - t_start) / 60:.1f} min)", file=sys.stderr, flush=True)
     for (c, s) in alts:
