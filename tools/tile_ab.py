@@ -42,6 +42,10 @@ LOOP = [("gru04.conv0", 384, 384, 3, 120, 160), ("gru04.conv1", 512, 512, 3, 120
 # (name, C, D, H, W): Conv3dNormActReduced.conv2 at cfg2 (D4 = 48 at 120 x 160)
 DEPTH = [("conv_out", 28, 48, 120, 160), ("agg_1", 56, 24, 60, 80), ("agg_0", 112, 12, 30, 40),
          ("conv3", 168, 6, 15, 20)]
+# (name, cin, cout, kd, k, D, H, W): the volume convs of corr_stem / classifier / Conv3dNormActReduced.conv1
+VOL = [("stem3x3x3", 28, 28, 3, 3, 48, 120, 160), ("cls3x3x3", 28, 14, 3, 3, 48, 120, 160),
+       ("cls14", 14, 14, 3, 3, 48, 120, 160), ("red1x3x3", 28, 28, 1, 3, 48, 120, 160),
+       ("agg1_1x3x3", 56, 56, 1, 3, 24, 60, 80)]
 
 
 def graph_time(fn):
@@ -109,6 +113,25 @@ if a.set in ("depth", "all"):
         tcfg, tns = ops._tuned(1, 17, C, C, 1, D, H, W, -1, -1)
         fl = 2.0 * C * C * 17 * D * H * W
         for cfg, ns in [(30, 1), (tcfg, tns), (7, 1), (4, 1)]:
+            fn = lambda: ops.conv3d(x, pk, bias=b, act="relu", cfg=cfg, nsplit=ns)  # noqa: E731
+            us = graph_time(fn)
+            r = {"layer": name, "cfg": cfg, "nsplit": ns, "us": round(us, 2), "TF": round(fl / us / 1e6, 1),
+                 "rel_err": rel(fn(), ref)}
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+if a.set in ("vol", "all"):
+    for name, cin, cout, kd, k, D, H, W in VOL:
+        if a.only and name not in a.only.split(","):
+            continue
+        gen = torch.Generator(device="cpu").manual_seed(cin + cout + kd)
+        x = torch.randn(1, cin, D, H, W, generator=gen).to(dev)
+        w = (torch.randn(cout, cin, kd, k, k, generator=gen) * 0.05).to(dev)
+        b = torch.randn(cout, generator=gen).to(dev)
+        pk = ops.PackedConv(w, mode="halo")
+        ref = F.relu(F.conv3d(x.double(), w.double(), b.double(), padding=(kd // 2, k // 2, k // 2)))
+        tcfg, tns = ops._tuned(k, kd, cin, cout, 1, D, H, W, -1, -1)
+        fl = 2.0 * cin * cout * kd * k * k * D * H * W
+        for cfg, ns in [(tcfg, tns), (7, 1), (6, 1), (5, 1), (23, 1)]:
             fn = lambda: ops.conv3d(x, pk, bias=b, act="relu", cfg=cfg, nsplit=ns)  # noqa: E731
             us = graph_time(fn)
             r = {"layer": name, "cfg": cfg, "nsplit": ns, "us": round(us, 2), "TF": round(fl / us / 1e6, 1),
