@@ -138,4 +138,17 @@ if a.set in ("vol", "all"):
                  "rel_err": rel(fn(), ref)}
             rows.append(r)
             print(json.dumps(r), flush=True)
+if a.set in ("cls", "all"):
+    # the classifier head Conv3d(14, 1, 7) (fp32 FMA direct kernel) at cfg2 / cfg3-per-GPU
+    for name, B, D, H, W in [("cls7_cfg2", 1, 48, 120, 160), ("cls7_b4", 4, 48, 120, 160)]:
+        gen = torch.Generator(device="cpu").manual_seed(7)
+        x = torch.randn(B, 14, D, H, W, generator=gen).to(dev)
+        w = (torch.randn(1, 14, 7, 7, 7, generator=gen) * 0.05).to(dev)
+        b = torch.randn(1, generator=gen).to(dev)
+        ref = F.conv3d(x.double(), w.double(), b.double(), padding=3)
+        fl = 2.0 * 14 * 343 * B * D * H * W
+        fn = lambda: ops.conv3d_direct(x, w, b)  # noqa: E731
+        us = graph_time(fn)
+        r = {"layer": name, "us": round(us, 2), "TF": round(fl / us / 1e6, 1), "rel_err": rel(fn(), ref)}
+        print(json.dumps(r), flush=True)
 ops.range_overflowed(reset=True)
