@@ -120,10 +120,14 @@ def test_conv_tuning_db_wellformed():
         ks, kd, cin, cout, B, D, H, W = (int(v) for v in re.findall(r"\d+", key))
         assert key == ops._tune_key(ks, kd, cin, cout, B, D, H, W)
         assert ks in (1, 3) and kd % 2 == 1 and min(cin, cout, B, D, H, W) > 0
-        # plain tiles 0..9 (all legal on volumes too), the K-group variants 16 + 3/4/5/7, or the
-        # pointwise tiles 24..26 (2D 1x1 layers only)
+        # plain tiles 0..9 (all legal on volumes too), the K-group variants 16 + 3/4/5/7, the
+        # pointwise tiles 24..26 (2D 1x1 layers only), the depth-blocked (17, 1, 1) tile 30, or the
+        # pipelined-staging register tiles 32 + (2..9) (conv_halo_x3.hip: volumes fall back to the
+        # plain tile)
         assert (0 <= e["cfg"] <= 9 or e["cfg"] in (19, 20, 21, 23)
-                or (24 <= e["cfg"] <= 26 and ks == 1 and kd == 1 and D == 1)) and 1 <= e["nsplit"] <= 8, (key, e)
+                or (24 <= e["cfg"] <= 26 and ks == 1 and kd == 1 and D == 1)
+                or (e["cfg"] == 30 and kd == 17 and ks == 1)
+                or 34 <= e["cfg"] <= 41) and 1 <= e["nsplit"] <= 8, (key, e)
 
 
 def test_lookup_channel_order():
