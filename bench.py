@@ -100,15 +100,15 @@ def cpu_baseline(args, H, W, iters, threads, hiera=False):
             def features(B, h, w):
                 fl, fr, vf = synth.backbone_features(B, h, w, args.vit_size, shift_px=8)
                 return [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr], torch.from_numpy(vf)
-            oracle.oracle_hierarchical(P, args, torch.from_numpy(left), torch.from_numpy(right), features,
+            out = oracle.oracle_hierarchical(P, args, torch.from_numpy(left), torch.from_numpy(right), features,
                                        iters=iters, timer=T)
         else:
             fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, shift_px=8)
-            oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
+            out = oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
                                   [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr],
                                   torch.from_numpy(vf), iters=iters, timer=T)
     dt = time.perf_counter() - t0
-    return dt, T.stages
+    return dt, T.stages, out
 
 
 def _cpu_model():
@@ -139,7 +139,11 @@ def main():
                     help="replay each rank's forward as one captured hipGraph (after eager warmup)")
     ap.add_argument("--conv-engine", default="fsmi", choices=["fsmi", "miopen"],
                     help="refinement-loop convs: halo-tiled split-precision MFMA kernels or MIOpen (A/B)")
+    ap.add_argument("--precision", default=os.environ.get("FSMI_PRECISION", "parity"), choices=["parity", "fast"],
+                    help="parity: 3 fp16 MFMA products per conv MAC (~22-bit split, the headline); fast: one "
+                         "fp16 product (the reference's fp16-autocast GPU precision; |dd| reported, not parity)")
     a = ap.parse_args()
+    os.environ["FSMI_PRECISION"] = a.precision      # read by _lib.load(): libfsmi.so / libfsmi_fast.so
     from foundationstereo_amd import update as fupdate
     fupdate.CONV_ENGINE = a.conv_engine
 
@@ -277,6 +281,7 @@ def main():
             traffic_build = pmc.get("build_hbm_bytes_per_launch")
 
     pairs = a.steps * B
+    nprod = 1 if a.precision == "fast" else 3      # fp16 MFMA products per conv MAC
     res = {
         "metric": f"stereo pairs/sec ({iters} refinement iters)",
         "value": pairs / elapsed,
@@ -290,8 +295,11 @@ def main():
         "vs_baseline": None,
         # fp32 arithmetic throughout; the convs run as 3 fp16 MFMA products per MAC on fp16 hi/lo
         # splits (~22-bit operand mantissas, fp32 accumulation), not as fp32 MFMA
-        "dtype": ("f32 (3xfp16 split MFMA convs; library convs fp16 under autocast)" if a.mixed_precision
+        "dtype": ("fp16 convs (1 fp16 MFMA product per MAC, fp32 accumulate; fp32 volumes + lookup)"
+                  if a.precision == "fast" else
+                  "f32 (3xfp16 split MFMA convs; library convs fp16 under autocast)" if a.mixed_precision
                   else "f32 (3xfp16 split MFMA)"),
+        "precision": a.precision,
         "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
         "range_overflow": range_overflow,
         # forwards re-run in safe range mode after their range flag came back set (ops.guarded)
@@ -316,8 +324,8 @@ def main():
         # the step time; algorithmic = fp32 conv FLOPs, peak = dense fp16 MFMA / 3 products per MAC
         "roofline_conv": {"kernel": "conv*_halo_x3 (all halo convs: loop, 3D filter, context net)", "bound": "mfma",
                           "achieved": cv_flops / (cv_ms / 1e3) / 1e12 if cv_n else None,
-                          "peak": MFMA_F16_PEAK / 3 / 1e12, "unit": "TFLOP/s",
-                          "frac": cv_flops / (cv_ms / 1e3) / (MFMA_F16_PEAK / 3) if cv_n else None,
+                          "peak": MFMA_F16_PEAK / nprod / 1e12, "unit": "TFLOP/s",
+                          "frac": cv_flops / (cv_ms / 1e3) / (MFMA_F16_PEAK / nprod) if cv_n else None,
                           "algorithmic_flops": cv_flops, "total_ms": cv_ms, "launches": cv_n},
         "roofline_build": {"kernel": "comb_volume_stem", "bound": "hbm",
                            "achieved": cb_bytes / cb_avg / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
@@ -332,7 +340,11 @@ def main():
         # the host cores this process is given: OMP_NUM_THREADS (16 on the GPU box = its CPU share
         # per GPU; os.cpu_count() there reports the whole machine, shared with other jobs)
         threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1)
-        dt, stages = cpu_baseline(args, H, W, iters, threads, hiera=a.config in HIERA)
+        dt, stages, ref = cpu_baseline(args, H, W, iters, threads, hiera=a.config in HIERA)
+        # the oracle ran pair 0 of this very workload (same seeds): the step's own disparity vs it
+        dd = float((out[0].float().cpu() - ref[0].float()).abs().max())
+        res["parity"] = {"max_abs_dd_px": dd, "vs": "CPU oracle (fp32), pair 0 of the timed step's output",
+                         "tolerance_px": 1e-3, "ok": dd < 1e-3}
         res["cpu_baseline"] = {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
                                "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
                                "sample": f"1 pair of {a.config} (all {iters} iterations) through the fp32 "

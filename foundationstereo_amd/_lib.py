@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-from .build import LIB
+from .build import LIB, LIB_FAST
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -81,15 +81,32 @@ class FsmiError(RuntimeError):
     pass
 
 
+def precision() -> str:
+    """Conv arithmetic of this process: "parity" (default; 3 fp16 MFMA products per MAC on hi/lo
+    splits, ~22-bit operands, |dd| < 1e-3 px vs the fp32 CPU reference) or "fast" (FSMI_PRECISION=fast:
+    one fp16 product per MAC with fp32 accumulation -- the reference's own fp16-autocast GPU
+    precision, not within the parity tolerance).  Volumes, lookup and every non-conv kernel are fp32
+    in both."""
+    p = os.environ.get("FSMI_PRECISION", "parity").lower()
+    if p not in ("parity", "fast"):
+        raise FsmiError(f"FSMI_PRECISION={p!r}: 'parity' or 'fast'")
+    return p
+
+
+def library_path() -> str:
+    """FSMI_LIB (A/B builds of the same ABI, tools/), else the in-tree library of ``precision()``."""
+    return os.environ.get("FSMI_LIB") or (LIB_FAST if precision() == "fast" else LIB)
+
+
 def load():
     """Load libfsmi.so once; raise if it is absent (no CPU fallback exists)."""
     global _lib
     if _lib is not None:
         return _lib
-    path = os.environ.get("FSMI_LIB", LIB)   # A/B builds of the same ABI (tools/); default in-tree
+    path = library_path()
     if not os.path.exists(path):
-        raise FsmiError(f"libfsmi.so not found at {path}: the HIP hot path is not built "
-                        "(run `python -m foundationstereo_amd.build`)")
+        raise FsmiError(f"{os.path.basename(path)} not found at {path}: the HIP hot path is not built "
+                        "(run `python -m foundationstereo_amd.build`, or __graft_entry__.build())")
     lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name, None)

@@ -19,6 +19,10 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(REPO, "build", "fsmi")
 LIB_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIB_DIR, "libfsmi.so")
+# reference-precision variant (FSMI_PRECISION=fast): one fp16 MFMA product per MAC instead of the
+# 3-product split (csrc/conv_halo.h FSMI_NPROD); same ABI
+LIB_FAST = os.path.join(LIB_DIR, "libfsmi_fast.so")
+FAST_DEFINES = ("FSMI_NPROD=1",)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
@@ -72,6 +76,11 @@ def build_library(force: bool = False, verbose: bool = False, defines=(), varian
     if force or jobs or _stale(lib, objs):
         run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib])
     return lib
+
+
+def build_fast(force: bool = False, verbose: bool = False) -> str:
+    """The reference-precision library (one fp16 MFMA product per MAC), _lib/libfsmi_fast.so."""
+    return build_library(force=force, verbose=verbose, defines=FAST_DEFINES, variant="fast")
 
 
 if __name__ == "__main__":

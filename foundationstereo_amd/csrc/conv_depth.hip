@@ -158,8 +158,10 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
         const int slot = (U - j) & 7;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][1], bh[k], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][0], bl[k], acc[j], 0, 0, 0);
+          if constexpr (FSMI_NPROD == 3) {
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][1], bh[k], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][0], bl[k], acc[j], 0, 0, 0);
+          }
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][0], bh[k], acc[j], 0, 0, 0);
         }
       }

@@ -59,6 +59,15 @@ constexpr int range_mode() { return FSMI_HALO_RANGE == 1 ? (D3 ? 1 : 2) : FSMI_H
 #ifndef FSMI_WREG_BPREF
 #define FSMI_WREG_BPREF 1                            // 0: A/B build, B fragments read just before their MFMAs
 #endif
+// MFMA products per MAC: 3 (default) = hi*hi + hi*lo + lo*hi, the ~22-bit split that keeps the
+// fp32 parity (|dd| < 1e-3 px); 1 = hi*hi only -- one fp16 product with fp32 accumulation, the
+// precision of the reference's own GPU path (fp16 autocast, scripts/run_demo.py:161).  The 1-product
+// build is a separate library (libfsmi_fast.so, FSMI_PRECISION=fast): lo halves are neither
+// computed nor stored, lo weight fragments never loaded.
+#ifndef FSMI_NPROD
+#define FSMI_NPROD 3
+#endif
+static_assert(FSMI_NPROD == 1 || FSMI_NPROD == 3, "FSMI_NPROD: 1 or 3 MFMA products per MAC");
 #ifndef FSMI_HALO_PERCOUT
 #define FSMI_HALO_PERCOUT 1                          // 0: A/B build reading one weight scale (row 0's)
 #endif
@@ -508,9 +517,11 @@ struct HaloStage {
           ovf |= m >= 65504.f;                    // (an inf input flags too; NaN is ignored by fmax)
         }
         const half8 hi = __builtin_convertvector(x, half8);
-        const half8 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x8), half8);
         *reinterpret_cast<half8*>(&Xh[hp][g * 8]) = hi;
-        *reinterpret_cast<half8*>(&Xl[hp][g * 8]) = lo;
+        if constexpr (FSMI_NPROD == 3) {
+          const half8 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x8), half8);
+          *reinterpret_cast<half8*>(&Xl[hp][g * 8]) = lo;
+        }
       }
     }
   }
@@ -649,8 +660,10 @@ __device__ __forceinline__ void mma3(f32x16 (&acc)[TM][TN], const half8 (&ah)[TM
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      if constexpr (FSMI_NPROD == 3) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      }
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
     }
 }

@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
         }
         ovf |= mx >= 65504.f;
         bh[j] = __builtin_convertvector(x, half8);
-        bl[j] = __builtin_convertvector(x - __builtin_convertvector(bh[j], f32x8), half8);
+        if constexpr (FSMI_NPROD == 3) bl[j] = __builtin_convertvector(x - __builtin_convertvector(bh[j], f32x8), half8);
       }
       mma3<TM, TN>(acc, ah, al, bh, bl);
     }

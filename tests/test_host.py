@@ -50,6 +50,26 @@ def test_library_exports_header_symbols():
     assert lib.fsmi_version() >= 100
 
 
+def test_fast_library_same_abi(monkeypatch):
+    """libfsmi_fast.so (FSMI_PRECISION=fast: one fp16 MFMA product per conv MAC) is a separate build of
+    the same C ABI, selected by _lib.library_path(); an unknown precision is refused."""
+    import ctypes
+    from foundationstereo_amd import _lib, build
+    monkeypatch.delenv("FSMI_LIB", raising=False)
+    monkeypatch.setenv("FSMI_PRECISION", "fast")
+    assert _lib.library_path() == build.LIB_FAST
+    if not os.path.exists(build.LIB_FAST):
+        pytest.skip("fast library not built")
+    lib = ctypes.CDLL(build.LIB_FAST)
+    for s in _header_symbols():
+        assert hasattr(lib, s), s
+    monkeypatch.setenv("FSMI_PRECISION", "parity")
+    assert _lib.library_path() == build.LIB
+    monkeypatch.setenv("FSMI_PRECISION", "bf16")
+    with pytest.raises(_lib.FsmiError, match="FSMI_PRECISION"):
+        _lib.precision()
+
+
 def test_library_rejects_bad_args_without_gpu():
     """Argument validation happens before any HIP call, so it is testable on the CPU."""
     from foundationstereo_amd import _lib
