@@ -307,131 +307,6 @@ __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
   clock_end(a.clk);
 }
 
-// a6, 4 pixels per lane (W % 4 == 0, 16-B aligned pyramids, disparity and output): grid =
-// (ceil(P/256), L, nchunk/4); lane = 4 consecutive pixels of one row, wave = 256 pixels x one chunk
-// of 4 geo channels (or the corr channel).  Every tap is the same fp32 expression as
-// geo_lookup_kernel (Taps<R> per pixel), so the two kernels agree bit for bit.  What changes is the
-// memory-instruction count per pixel and channel: where the disparity field is smooth (the 4
-// pixels' windows start within one depth row of each other) the union of their windows is 2r+5
-// depth rows, each ONE 16-B load for the 4 pixels (2r+5 dwordx4 loads instead of 4 x (2r+4) dword
-// gathers), and the 2r+1 taps leave as 16-B stores (instead of 4 x (2r+1) dword stores).  Lanes
-// whose windows spread further (disparity edges) gather per pixel as the scalar kernel does.
-// Taps<R>::init's values with the per-tap window offsets packed two bits each (sel in {0, 1, 2}):
-// four pixels' taps held across the channel loop in 4 x (2 + 2r+1) registers instead of 4 x (4r+3)
-template <int R>
-struct TapsPacked {
-  static constexpr int K = 2 * R + 1;
-  int xb;
-  unsigned selp;
-  float f[K];
-  __device__ __forceinline__ void init(float xc, int n) {
-    Taps<R> t;
-    t.init(xc, n);
-    xb = t.xb;
-    selp = 0u;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      f[k] = t.f[k];
-      selp |= static_cast<unsigned>(t.sel[k]) << (2 * k);
-    }
-  }
-  __device__ __forceinline__ int sel(int k) const { return static_cast<int>((selp >> (2 * k)) & 3u); }
-};
-
-#ifndef FSMI_LOOKUP_V4_UNROLL
-#define FSMI_LOOKUP_V4_UNROLL 1                    // channels whose row loads are in flight together
-#endif
-template <int R>
-__global__ __launch_bounds__(256) void geo_lookup_v4_kernel(LookupArgs a) {
-  constexpr int K = 2 * R + 1, NW = 2 * R + 4, NR = NW + 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = blockIdx.y;  // level
-  clock_begin(a.clk);
-  const int chunk = blockIdx.z * 4 + wave;
-  const int nchunk_geo = (a.Cv + kCPC - 1) / kCPC;
-  if (chunk > nchunk_geo) return;
-  const int HW = a.H * a.W;
-  const long long p = (static_cast<long long>(blockIdx.x) * 64 + lane) * 4;   // first of 4 pixels
-  if (p >= static_cast<long long>(a.B) * HW) return;
-  const int b = static_cast<int>(p / HW);
-  const int hw = static_cast<int>(p - static_cast<long long>(b) * HW);
-  const int w = hw % a.W;
-  const float s = static_cast<float>(1 << i);
-  const float4 dv = *reinterpret_cast<const float4*>(a.disp + p);
-  const float ds[4] = {dv.x / s, dv.y / s, dv.z / s, dv.w / s};
-  const int CH = a.L * K * (a.Cv + 1);
-  const int base = i * K * (a.Cv + 1);
-  float* outp = a.out + static_cast<size_t>(b) * CH * HW + hw;
-  if (chunk < nchunk_geo) {
-    const int Di = a.D >> i;
-    TapsPacked<R> tp[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tp[q].init(ds[q], Di);
-    const int xmin = min(min(tp[0].xb, tp[1].xb), min(tp[2].xb, tp[3].xb));
-    const int xmax = max(max(tp[0].xb, tp[1].xb), max(tp[2].xb, tp[3].xb));
-    const float* vol = a.vol[i] + static_cast<size_t>(b) * a.Cv * Di * HW + hw;
-    const int c0 = chunk * kCPC, c1 = min(c0 + kCPC, a.Cv);
-    if (xmax - xmin <= 1) {
-      // slot j of pixel q's window = union row j + o[q]; tap k reads slots k + sel and k + sel + 1,
-      // i.e. union rows k + u and k + u + 1 with u = sel + o in 0..3
-      int o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = tp[q].xb - xmin;
-#pragma unroll FSMI_LOOKUP_V4_UNROLL
-      for (int c = c0; c < c1; ++c) {
-        const float* src = vol + static_cast<size_t>(c) * Di * HW;
-        float4 row[NR];
-#pragma unroll
-        for (int j = 0; j < NR; ++j) {
-          const int x = xmin + j;
-          row[j] = (x >= 0 && x < Di) ? *reinterpret_cast<const float4*>(src + static_cast<size_t>(x) * HW)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        float* dst = outp + static_cast<size_t>(base + c * K) * HW;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            auto comp = [q](const float4& f) { return q == 0 ? f.x : (q == 1 ? f.y : (q == 2 ? f.z : f.w)); };
-            const int uq = tp[q].sel(k) + o[q];
-            const float r0 = comp(row[k]), r1 = comp(row[k + 1]), r2 = comp(row[k + 2]), r3 = comp(row[k + 3]),
-                        r4 = comp(row[k + 4]);
-            const float v0 = uq == 0 ? r0 : (uq == 1 ? r1 : (uq == 2 ? r2 : r3));
-            const float v1 = uq == 0 ? r1 : (uq == 1 ? r2 : (uq == 2 ? r3 : r4));
-            {
-#pragma clang fp contract(off)
-              v[q] = v0 * (1.f - tp[q].f[k]) + v1 * tp[q].f[k];
-            }
-          }
-          *reinterpret_cast<float4*>(dst + static_cast<size_t>(k) * HW) = make_float4(v[0], v[1], v[2], v[3]);
-        }
-      }
-    } else {
-      // spread windows (disparity edges): the scalar kernel's gather, one pixel at a time
-#pragma unroll 1
-      for (int q = 0; q < 4; ++q) {
-        Taps<R> t;                                  // recomputed: the packed taps stay compact
-        t.init(ds[q], Di);
-        for (int c = c0; c < c1; ++c)
-          t.sample(vol + static_cast<size_t>(c) * Di * HW + q, HW, Di, outp + static_cast<size_t>(base + c * K) * HW + q,
-                   HW);
-      }
-    }
-  } else {
-    const int W2i = a.W2 >> i;
-    float* dst = outp + static_cast<size_t>(base + a.Cv * K) * HW;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      Taps<R> t;
-      t.init(static_cast<float>(w + q) / s - ds[q], W2i);
-      t.sample(a.cor[i] + static_cast<size_t>(p + q) * W2i, 1, W2i, dst + q, HW);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  clock_end(a.clk);
-}
-
 // bilinear_sampler 1-D: img (P,C,1,Lx), x (P,K) -> out (P,C,1,K)
 __global__ __launch_bounds__(256) void sampler_kernel(const float* __restrict__ img, const float* __restrict__ xs,
                                                       float* __restrict__ out, int C, int Lx, int K,
@@ -534,26 +409,10 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
   a.B = B;
   const long long P = static_cast<long long>(B) * H * W;
   const int nchunk = (Cv + kCPC - 1) / kCPC + 1;
-  // 4 pixels per lane (geo_lookup_v4_kernel) when rows split into aligned quads: W % 4 == 0 and
-  // 16-B aligned level / disparity / output bases; FSMI_LOOKUP_V4=0 keeps the scalar kernel (A/B)
-  const char* v4e = std::getenv("FSMI_LOOKUP_V4");  // read per call (tests switch it in-process)
-  const int v4_env = v4e ? std::atoi(v4e) : 1;
-  auto al16 = [](const void* q) { return reinterpret_cast<uintptr_t>(q) % 16 == 0; };
-  bool v4 = v4_env != 0 && W % 4 == 0 && al16(disp) && al16(out);
-  for (int i = 0; i < num_levels; ++i) v4 = v4 && al16(a.vol[i]);
-  const int ppb = v4 ? 256 : 64;                   // pixels per block
-  dim3 grid(ceil_div(P, ppb), num_levels, (nchunk + 3) / 4);
+  dim3 grid(ceil_div(P, 64), num_levels, (nchunk + 3) / 4);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_LOOKUP, s);
-  auto launch = [grid, radius, s, v4](const LookupArgs& la) {
-    if (v4) {
-      switch (radius) {
-        case 2: hipLaunchKernelGGL(geo_lookup_v4_kernel<2>, grid, dim3(256), 0, s, la); break;
-        case 3: hipLaunchKernelGGL(geo_lookup_v4_kernel<3>, grid, dim3(256), 0, s, la); break;
-        default: hipLaunchKernelGGL(geo_lookup_v4_kernel<4>, grid, dim3(256), 0, s, la); break;
-      }
-      return;
-    }
+  auto launch = [grid, radius, s](const LookupArgs& la) {
     switch (radius) {
       case 2: hipLaunchKernelGGL(geo_lookup_kernel<2>, grid, dim3(256), 0, s, la); break;
       case 3: hipLaunchKernelGGL(geo_lookup_kernel<3>, grid, dim3(256), 0, s, la); break;

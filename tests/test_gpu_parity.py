@@ -651,35 +651,6 @@ def test_lookup_vs_oracle(ops_mod, L, D, W):
     close(out, ref(t(disp), coords), atol=1e-5)
 
 
-@pytest.mark.parametrize("L,D,W,B", [(4, 48, 160, 2), (2, 16, 40, 1), (4, 80, 96, 1), (3, 48, 64, 1)])
-def test_lookup_v4_bit_exact(ops_mod, monkeypatch, L, D, W, B):
-    """geo_lookup_v4_kernel (4 pixels per lane, 16-B row loads where the windows are within one row)
-    against the scalar kernel: identical fp32 expressions, so bit-equal.  The disparity field mixes
-    smooth rows (the vector path), rough rows (spread windows: the per-pixel fallback), integer and
-    out-of-range values."""
-    Cv, H = 28, 6
-    vol = g(synth.normal(65, (B, Cv, D, H, W)))
-    f1, f2 = g(synth.normal(66, (B, 64, H, W))), g(synth.normal(67, (B, 64, H, W)))
-    corr = ops_mod.allpairs_corr(f1, f2, L)
-    pyr = ops_mod.volume_pyramid(vol, L)
-    ww = np.arange(W, dtype=np.float32)
-    disp = np.empty((B, 1, H, W), np.float32)
-    for b in range(B):
-        disp[b, 0, 0] = 0.3 * D + 0.2 * D * ww / W                         # smooth
-        disp[b, 0, 1] = synth.uniform(68 + b, (W,), -8.0, D + 8.0)          # rough
-        disp[b, 0, 2] = np.round(0.5 * D + 3 * np.sin(ww / 5))              # integers
-        disp[b, 0, 3] = np.where(ww % 8 < 4, -3.5, D + 2.25)                # out of range
-        disp[b, 0, 4] = 0.5 * D + 0.9 * np.sin(ww)                         # spread of ~1 row
-        disp[b, 0, 5] = 7.0 + (ww % 4) * 0.49                               # windows 0/1 rows apart
-    dg = g(disp)
-    monkeypatch.setenv("FSMI_LOOKUP_V4", "0")
-    ref = ops_mod.geo_lookup(pyr, corr, dg, 4)
-    monkeypatch.setenv("FSMI_LOOKUP_V4", "1")
-    out = ops_mod.geo_lookup(pyr, corr, dg, 4)
-    torch.cuda.synchronize()
-    assert torch.equal(out, ref), float((out - ref).abs().max())
-
-
 def test_bilinear_sampler_golden(ops_mod, gold):
     from foundationstereo_amd.utils import bilinear_sampler
     close(bilinear_sampler(g(gold["bs_img"]), g(gold["bs_coords"])), gold["bs_out"])
