@@ -327,6 +327,13 @@ def main():
                           "peak": MFMA_F16_PEAK / nprod / 1e12, "unit": "TFLOP/s",
                           "frac": cv_flops / (cv_ms / 1e3) / (MFMA_F16_PEAK / nprod) if cv_n else None,
                           "algorithmic_flops": cv_flops, "total_ms": cv_ms, "launches": cv_n},
+        # the same conv FLOPs over the graph-replayed step's wall time (every other kernel of the step
+        # included, the 4-stream overlap on): a lower bound on the convs' in-step rate -- the
+        # single-stream figure above leaves the CUs idle that low-block-count layers do not fill
+        "roofline_conv_step": {"achieved": cv_flops / (elapsed / a.steps) / 1e12 if cv_n else None,
+                               "peak": MFMA_F16_PEAK / nprod / 1e12, "unit": "TFLOP/s",
+                               "frac": cv_flops / (elapsed / a.steps) / (MFMA_F16_PEAK / nprod) if cv_n else None,
+                               "timed_over": "timed region (whole step)"},
         "roofline_build": {"kernel": "comb_volume_stem", "bound": "hbm",
                            "achieved": cb_bytes / cb_avg / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
                            "unit": "GB/s", "frac": cb_bytes / cb_avg / HBM_PEAK if cb_n else None,
