@@ -29,12 +29,6 @@
 namespace fsmi {
 namespace {
 
-#ifndef FSMI_DEPTH_NSET
-#define FSMI_DEPTH_NSET 2          // pipelined walk: plane register sets (2 or 4; 4 spills 44 B)
-#endif
-#ifndef FSMI_DEPTH_PIPE
-#define FSMI_DEPTH_PIPE 1          // 0: A/B build with the two-barrier plane walk (round 3 first version)
-#endif
 constexpr int kDepthDB = 16;        // output depths per block
 constexpr int kDepthTR = 2;        // pixel rows per block (x 32 columns)
 
@@ -51,14 +45,7 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
   __shared__ __attribute__((aligned(16))) _Float16 Wl[KD][32][32];
   __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
   __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
-#if !FSMI_DEPTH_PIPE
   __shared__ __attribute__((aligned(16))) float red[4];
-#else
-  // pipelined plane walk: a second plane buffer and a maxima slot per buffer parity
-  __shared__ __attribute__((aligned(16))) _Float16 Xh2[HS::NHP][HROW];
-  __shared__ __attribute__((aligned(16))) _Float16 Xl2[HS::NHP][HROW];
-  __shared__ __attribute__((aligned(16))) float red2[2][4];
-#endif
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = wave & 1, jh = wave >> 1;
@@ -81,11 +68,6 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
   HS hs, hs2;
   hs.init(a, tid, r0, c0);
   hs2.init(a, tid, r0, c0);
-#if FSMI_DEPTH_PIPE && FSMI_DEPTH_NSET == 4
-  HS hs3, hs4;
-  hs3.init(a, tid, r0, c0);
-  hs4.init(a, tid, r0, c0);
-#endif
   f32x16 acc[JW];
 #pragma unroll
   for (int j = 0; j < JW; ++j)
@@ -128,117 +110,6 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
     __syncthreads();               // the weight slab is visible
 #pragma unroll
     for (int j = 1; j < 8; ++j) read_tap(ra[(8 - j) & 7], p_lo - jbase + PD - j);
-#if FSMI_DEPTH_PIPE
-    // Pipelined plane walk (one barrier per plane).  Plane t = p_lo + t lives in register set t % NS
-    // (loaded NS + 1 planes ahead of its MFMAs), LDS buffer t & 1 and maxima slot t & 1.  Iteration t
-    // runs plane t's MFMAs; after them (VALU / LDS / memory, independent of the MFMAs) it fixes plane
-    // t+1's exponent from the maxima published before the previous barrier, splits and stores plane
-    // t+1 into the other buffer, loads plane t+NS+1 and publishes plane t+2's wave maxima.  The exponent
-    // arithmetic and the accumulator rescale (after plane t's products, before plane t+1's) are those
-    // of the two-barrier walk, so both produce the same sums.  Buffer / slot reuse is two planes
-    // apart, i.e. always across a barrier every wave has passed.
-    const int n = p_hi - p_lo + 1;
-    auto set_exp = [&](float bm) FSMI_HALO_INL {
-      ovf |= !(bm <= 3.4e38f);
-      const int fit = __builtin_amdgcn_readfirstlane(chunk_exp(bm));
-      if (fit != kNoExp && (fit < sx || (sx != kNoExp && fit > sx + 8))) {
-        int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom1>(bm));
-        if (sx != kNoExp) {
-          se = min(se, smin + 60);
-          const float f = exp2i(se - sx);
-#pragma unroll
-          for (int j = 0; j < JW; ++j) acc[j] *= f;
-        }
-        sx = se;
-        smin = min(smin, se);
-      }
-    };
-    constexpr int NS = FSMI_DEPTH_NSET;            // planes in registers: loaded NS + 1 ahead of their MFMAs
-    hs.load(a, b, cc, p_lo);
-    if (n > 1) hs2.load(a, b, cc, p_lo + 1);
-#if FSMI_DEPTH_NSET == 4
-    if (n > 2) hs3.load(a, b, cc, p_lo + 2);
-    if (n > 3) hs4.load(a, b, cc, p_lo + 3);
-#endif
-    {
-      const float m0 = wave_max(hs.absmax());
-      const float m1 = n > 1 ? wave_max(hs2.absmax()) : 0.f;
-      if (lane == 0) {
-        red2[0][wave] = m0;
-        red2[1][wave] = m1;
-      }
-    }
-    __syncthreads();               // plane 0 / 1 maxima visible
-    set_exp(red4_max(red2[0]));
-    hs.template store<1>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
-    if (n > NS) hs.load(a, b, cc, p_lo + NS);
-    __syncthreads();               // plane 0 staged
-    auto planep = [&](auto u_c, int t) FSMI_HALO_INL {
-      constexpr int U = decltype(u_c)::value;      // t & 7
-#if FSMI_DEPTH_NSET == 4
-      HS& nxt = U % 4 == 0 ? hs2 : (U % 4 == 1 ? hs3 : (U % 4 == 2 ? hs4 : hs));     // plane t + 1
-      HS& ahd = U % 4 == 0 ? hs3 : (U % 4 == 1 ? hs4 : (U % 4 == 2 ? hs : hs2));     // plane t + 2
-#else
-      HS& nxt = (U & 1) ? hs : hs2;                // plane t + 1
-      HS& ahd = (U & 1) ? hs2 : hs;                // plane t + 2
-#endif
-      _Float16 (*Rh)[HROW] = (U & 1) ? Xh2 : Xh;   // plane t
-      _Float16 (*Rl)[HROW] = (U & 1) ? Xl2 : Xl;
-      _Float16 (*Wh_)[HROW] = (U & 1) ? Xh : Xh2;  // plane t + 1
-      _Float16 (*Wl_)[HROW] = (U & 1) ? Xl : Xl2;
-      const int p = p_lo + t;
-      read_tap(ra[U], p - jbase + PD);             // output 0's new tap
-      half8 bh[2], bl[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        bh[k] = *reinterpret_cast<const half8*>(&Rh[row * 32 + rl][16 * k + 8 * hsel]);
-        bl[k] = *reinterpret_cast<const half8*>(&Rl[row * 32 + rl][16 * k + 8 * hsel]);
-      }
-#pragma unroll
-      for (int jj = 0; jj < JW; ++jj) {
-        const int j = JW - 1 - jj;
-        const int kd = p - jbase + PD - j;
-        if (kd < 0 || kd >= KD) continue;          // wave-uniform
-        const int slot = (U - j) & 7;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          if constexpr (FSMI_NPROD == 3) {
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][1], bh[k], acc[j], 0, 0, 0);
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][0], bl[k], acc[j], 0, 0, 0);
-          }
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[slot][k][0], bh[k], acc[j], 0, 0, 0);
-        }
-      }
-      if (t + 1 < n) {
-        set_exp(red4_max(red2[(U + 1) & 1]));
-        nxt.template store<1>(Wh_, Wl_, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
-        if (t + NS + 1 < n) nxt.load(a, b, cc, p + NS + 1);
-        if (t + 2 < n) {
-          const float m = wave_max(ahd.absmax());
-          if (lane == 0) red2[U & 1][wave] = m;
-        }
-      }
-      __syncthreads();             // plane t + 1 staged, plane t + 2 maxima visible
-    };
-    for (int t = 0; t < n; t += 8) {
-      planep(std::integral_constant<int, 0>(), t);
-      if (t + 1 >= n) break;
-      planep(std::integral_constant<int, 1>(), t + 1);
-      if (t + 2 >= n) break;
-      planep(std::integral_constant<int, 2>(), t + 2);
-      if (t + 3 >= n) break;
-      planep(std::integral_constant<int, 3>(), t + 3);
-      if (t + 4 >= n) break;
-      planep(std::integral_constant<int, 4>(), t + 4);
-      if (t + 5 >= n) break;
-      planep(std::integral_constant<int, 5>(), t + 5);
-      if (t + 6 >= n) break;
-      planep(std::integral_constant<int, 6>(), t + 6);
-      if (t + 7 >= n) break;
-      planep(std::integral_constant<int, 7>(), t + 7);
-    }
-  }
-#else
     hs.load(a, b, cc, p_lo);
     if (p_lo + 1 <= p_hi) hs2.load(a, b, cc, p_lo + 1);
     // plane p = p_lo + 8 g + U, staged from register set st (loaded two planes ahead)
@@ -313,7 +184,6 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
       plane(std::integral_constant<int, 7>(), hs2, p + 7);
     }
   }
-#endif
   flag_overflow(a, ovf);
   const float xinv = exp2i(sx == kNoExp ? 0 : -sx);
   const int hh = r0 + row, ww = c0 + rl;
