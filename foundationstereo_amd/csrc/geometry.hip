@@ -242,16 +242,16 @@ __global__ __launch_bounds__(256) void volume_pyramid_kernel(const float* __rest
 
 // ---------------------------------------------------------------------------
 // a6: fused lookup.  grid = (ceil(P/64), L, nchunk/4); one wave = 64
-// consecutive pixels x one chunk of kCPC = 7 geo channels (or the corr channel)
-// of one level: Cv = 28 -> 4 geo waves + 1 corr wave per (pixel run, level)
-// (7 vs 4 per wave: 36.5 vs 37.4 us at cfg2, same step time; 2 per wave 37.9).  Coordinates follow bilinear_sampler: x -> 2x/(n-1)-1 -> (x'+1)
+// consecutive pixels x one chunk of kCPC = 4 geo channels (or the corr channel)
+// of one level.  (7 per wave: 36.5 vs 37.4 us alone at cfg2 but 44.2 vs 42.0 us
+// average inside the concurrent loop under rocprof; 2 per wave 37.9 us.)  Coordinates follow bilinear_sampler: x -> 2x/(n-1)-1 -> (x'+1)
 // * ((n-1)/2) (the CPU grid_sampler's align_corners unnormalise), then linear
 // interpolation with zero padding.  The 2r+4 window around floor(x) is loaded
 // once per channel into registers; each tap selects its pair with
 // compile-time indices (no scratch), so a channel costs 2r+4 loads, not 4r+2.
 // ---------------------------------------------------------------------------
 #ifndef FSMI_LOOKUP_CPC
-#define FSMI_LOOKUP_CPC 7
+#define FSMI_LOOKUP_CPC 4
 #endif
 constexpr int kCPC = FSMI_LOOKUP_CPC;  // geo channels per wave
 
