@@ -581,7 +581,10 @@ __device__ __forceinline__ int chunk_exp(float m) {
 // range mode 2: the block's first chunk fixes its exponent with 8 bits of headroom, so later
 // chunks up to 2^9 x larger still fit fp16; a value beyond that raises the range flag instead
 // (fsmi_range_status) -- no per-chunk reduction and no accumulator rescale in the main loop.
-constexpr int kRangeHeadroom = 8;
+// The one-product build (FSMI_NPROD = 1) keeps no lo half, so its hi half holds fp16's 11 bits for
+// any value in fp16's normal range whatever the scale: there the first chunk's maximum is aimed at
+// [2, 4) (13 bits of headroom), so later chunks up to 2^14 x larger still fit.
+constexpr int kRangeHeadroom = FSMI_NPROD == 1 ? 13 : 8;
 
 __device__ __forceinline__ void flag_overflow(const HaloArgs& a, bool ovf) {
   if (ovf && a.ovf) *a.ovf = 1;    // vector store from the lanes that saw one (same value, benign race)
