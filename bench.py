@@ -199,8 +199,13 @@ def main():
     if rank == 0:
         print(f"[bench] setup {t_warm - t_setup:.1f}s warmup {time.perf_counter() - t_warm:.1f}s", file=sys.stderr)
     if a.graph:
+        # the captured lookups carry the in-kernel clock (timer mode 2): after the timed replays their
+        # stamps hold the last replay's launches, i.e. the lookup as it runs inside the timed step,
+        # beside the other streams' convs (what rocprof's per-launch average of this command sees)
+        ops.timer_enable(True, in_capture=True)
         with torch.no_grad():
             runner.capture(batch)
+        ops.timer_enable(False)
         step()
         torch.cuda.synchronize()
     else:
@@ -220,6 +225,7 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+    lk_step_ms, lk_step_n = ops.timer_query_clock("lookup") if a.graph else (0.0, 0)
     if a.graph:
         # graph replays carry no per-kernel events (HIP rejects external event nodes during
         # capture): time the kernels over one eager pass of the identical step instead, on one
@@ -258,6 +264,9 @@ def main():
     #   arguments, same stream, identical outputs), which amortises the event latency.
     REPS = 20
     lk_rep = lk_ck_ms / lk_ck_n if lk_ck_n == lk_n and lk_n else None
+    lk_single = lk_rep                                 # single-stream eager pass, kernel clock
+    if lk_step_n:                                      # the timed step's own lookups (in-kernel clock)
+        lk_rep = lk_step_ms / lk_step_n
     cb_rep = ops.timer_replay("comb", REPS) if cb_n else None
     ops.timer_enable(False)
 
@@ -311,13 +320,19 @@ def main():
                    "corr_levels": L, "conv_engine": a.conv_engine, "hip_graph": bool(a.graph),
                    "parallelism": f"dp{world}"},
         "roofline": {"kernel": "geo_lookup", "bound": "hbm",
-                     "timed_over": ("single-stream eager step after the timed region" if a.graph else "timed region")
+                     "timed_over": ("timed region (last graph replay)" if lk_step_n else
+                                    "single-stream eager step after the timed region" if a.graph else "timed region")
                      + ("; standalone geo_lookup there, fused into convc1's staging in the timed step"
                         if fupdate.FUSE_LOOKUP else ""),
                      "achieved": lk_bytes / lk_avg / 1e9,
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
                      "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,
-                     "timed_by": "in-kernel clock over the eager step's launches" if lk_rep else "hip events",
+                     "timed_by": ("in-kernel clock of the lookups of the timed region's last graph replay "
+                                  "(4-stream step, other streams' convs sharing the chip)" if lk_step_n else
+                                  "in-kernel clock over the eager step's launches" if lk_rep else "hip events"),
+                     "avg_us_single_stream": lk_single * 1e3 if lk_single else None,
+                     "frac_single_stream": lk_bytes / (lk_single / 1e3) / HBM_PEAK if lk_single else None,
+                     "launches_in_step": lk_step_n,
                      "avg_us_events": lk_ev_ms * 1e3 / max(lk_n, 1),
                      "avg_us_kernel_clock": lk_ck_ms * 1e3 / max(lk_ck_n, 1), "launches": lk_n},
         # the refinement-loop convs (halo-tiled 3 x fp16 MFMA, split-K reduce included) hold most of

@@ -30,6 +30,7 @@ struct Pool {
 };
 std::mutex g_mu;
 bool g_enabled = false;
+bool g_clock_in_capture = false;   // fsmi_timer_enable(2): clock slots also inside stream capture
 Pool g_pool[FSMI_K_COUNT];
 
 bool take(int k, hipEvent_t* s, hipEvent_t* e) {
@@ -69,7 +70,10 @@ static int clock_init() {
 unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves) {
   if (!g_enabled || !g_clock || nwaves <= 0) return nullptr;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess) return nullptr;
+  // inside a capture the slot pointer is baked into the graph node: every replay overwrites the same
+  // stamps, so a query after replaying reads the last replay's launches (timer mode 2 only)
+  if (st != hipStreamCaptureStatusNone && !g_clock_in_capture) return nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
   const size_t need = 2 * static_cast<size_t>(nwaves);
   if (g_clock_top + need > kClockArena) return nullptr;
@@ -157,6 +161,7 @@ const char* fsmi_arch(void) { return "gfx950"; }
 int fsmi_timer_enable(int on) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   fsmi::g_enabled = on != 0;
+  fsmi::g_clock_in_capture = on == 2;
   for (auto& f : fsmi::g_replay) f = nullptr;      // a replay only targets buffers of the current session
   if (fsmi::g_enabled) {
     if (fsmi::clock_init() != FSMI_OK) {

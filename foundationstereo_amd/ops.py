@@ -880,8 +880,10 @@ def _keep_for_replay(kernel: str, *tensors):
         _REPLAY_KEEP[kernel] = tensors
 
 
-def timer_enable(on: bool = True):
-    _lib.check(_lib.load().fsmi_timer_enable(1 if on else 0), "timer_enable")
+def timer_enable(on: bool = True, in_capture: bool = False):
+    """Per-kernel timers on / off.  ``in_capture``: the lookup / build kernel clocks are also baked
+    into launches captured into a hipGraph (each replay rewrites them; query after replaying)."""
+    _lib.check(_lib.load().fsmi_timer_enable((2 if in_capture else 1) if on else 0), "timer_enable")
     _CONV_FLOPS["on"] = bool(on)
     _REPLAY_KEEP.clear()
 

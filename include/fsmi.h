@@ -337,6 +337,9 @@ int fsmi_set_range_safe(int safe);
 int fsmi_range_poison(float* out, long long n, void* stream);
 int fsmi_get_range_safe(int* safe);
 
+/* on: 0 off, 1 on (events + kernel clocks outside stream capture), 2 also the kernel clocks of
+ * launches captured into a hipGraph (their stamps are rewritten by every replay: a query after the
+ * replays reads the last replay's launches -- bench.py's in-step lookup timing). */
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
 int fsmi_timer_query(int kernel, double* total_ms, long long* count);
