@@ -1,0 +1,44 @@
+"""The measurement hooks bench.py reads (include/fsmi.h fsmi_timer_*): the in-kernel lookup clock,
+eagerly and -- timer mode 2 -- baked into a captured hipGraph, whose replays rewrite the stamps
+(bench.py's in-step roofline)."""
+import pytest
+import torch
+
+from foundationstereo_amd import synth
+
+
+@pytest.mark.gpu
+def test_lookup_clock_in_captured_graph():
+    from foundationstereo_amd import ops
+    dev = torch.device("cuda:0")
+    B, Cv, D, H, W, L = 1, 28, 48, 24, 64, 4
+    vol = torch.from_numpy(synth.normal(81, (B, Cv, D, H, W))).to(dev)
+    f1, f2 = (torch.from_numpy(synth.normal(s, (B, 64, H, W))).to(dev) for s in (82, 83))
+    corr = ops.allpairs_corr(f1, f2, L)
+    pyr = ops.volume_pyramid(vol, L)
+    disp = torch.from_numpy(synth.uniform(84, (B, 1, H, W), 0.0, D - 1.0)).to(dev)
+    ref = ops.geo_lookup(pyr, corr, disp, 4)
+    torch.cuda.synchronize()
+    try:
+        ops.timer_enable(True, in_capture=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = ops.geo_lookup(pyr, corr, disp, 4)
+            out2 = ops.geo_lookup(pyr, corr, disp, 4)
+        ops.timer_enable(False)
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        ms, n = ops.timer_query_clock("lookup")
+        assert n == 2 and 0.0 < ms / n < 5.0, (ms, n)       # both captured launches stamped, sane us
+        assert torch.equal(out, ref) and torch.equal(out2, ref)
+        # mode 1: captured launches carry no clock
+        ops.timer_enable(True)
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):
+            ops.geo_lookup(pyr, corr, disp, 4)
+        g2.replay()
+        torch.cuda.synchronize()
+        assert ops.timer_query_clock("lookup")[1] == 0
+    finally:
+        ops.timer_enable(False)
