@@ -202,10 +202,13 @@ def main():
         # the captured lookups carry the in-kernel clock (timer mode 2): after the timed replays their
         # stamps hold the last replay's launches, i.e. the lookup as it runs inside the timed step,
         # beside the other streams' convs (what rocprof's per-launch average of this command sees)
-        ops.timer_enable(True, in_capture=True)
+        step_clock = os.environ.get("FSMI_BENCH_STEP_CLOCK", "1") != "0"
+        if step_clock:
+            ops.timer_enable(True, in_capture=True)
         with torch.no_grad():
             runner.capture(batch)
-        ops.timer_enable(False)
+        if step_clock:
+            ops.timer_enable(False)
         step()
         torch.cuda.synchronize()
     else:
