@@ -122,6 +122,74 @@ def _cpu_model():
     return None
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` (N > 1) without a torchrun environment: start N ranks of this script, one
+    process per GPU, with torch.distributed.run on 127.0.0.1 and return their exit status.  This
+    parent process never initialises the GPU (no HIP call happens before this point) and does not
+    exec itself: the ranks are child processes."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def _world_info(world):
+    """(world_size, backend) as torch.distributed reports them (a single process has no group)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), str(dist.get_backend())
+    return world, "none (single process)"
+
+
+def dist_selftest(a):
+    """``--dist-selftest``: the launch / shard / gather / timing / reporting machinery of this bench
+    with a stand-in per-pair function on CPU tensors over gloo -- no model, no HIP kernels (the CPU
+    test of ``--gpus N``'s rank spawning, tests/test_bench_launch.py).  Its line says so in ``data``
+    and is not a measurement."""
+    rank, _, world = fdist.init_from_env("gloo")
+    wsz, backend = _world_info(world)
+    assert wsz == a.gpus, f"rank {rank}: world size {wsz} != --gpus {a.gpus}"
+    B, H, W = 2 * world, 16, 24
+    g = torch.Generator().manual_seed(7)
+    full = torch.rand(B, 2, 3, H, W, generator=g)
+    batch = full if rank == 0 else torch.zeros_like(full)
+    runner = fdist.ShardedStereo(lambda lf, rt: (lf - rt).abs().mean(1, keepdim=True), rank, world)
+    for _ in range(a.warmup):
+        runner.step(batch, (1, H, W))
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = runner.step(batch, (1, H, W))
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = bool(torch.allclose(out, (full[:, 0] - full[:, 1]).abs().mean(1, keepdim=True)))
+    if rank == 0:
+        print(json.dumps({"metric": "dist self-test (no model)", "value": a.steps * B / elapsed, "unit": "pairs/s",
+                          "n_gpus": wsz, "world_size": wsz, "backend": backend, "steps": a.steps,
+                          "warmup": a.warmup, "gathered_ok": ok,
+                          "data": "dist self-test: stand-in per-pair function on CPU tensors, not a measurement"}),
+              flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    assert ok, "gathered batch differs from the stand-in function"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,12 +210,26 @@ def main():
     ap.add_argument("--precision", default=os.environ.get("FSMI_PRECISION", "parity"), choices=["parity", "fast"],
                     help="parity: 3 fp16 MFMA products per conv MAC (~22-bit split, the headline); fast: one "
                          "fp16 product (the reference's fp16-autocast GPU precision; |dd| reported, not parity)")
+    ap.add_argument("--dist", action="store_true",
+                    help="create the torch.distributed process group (RCCL) even at one rank, so the step's "
+                         "scatter / all-gather run as collectives")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="CPU/gloo self-test of the rank launch and sharding machinery (no model, not a measurement)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    if a.dist_selftest:
+        return dist_selftest(a)
     os.environ["FSMI_PRECISION"] = a.precision      # read by _lib.load(): libfsmi.so / libfsmi_fast.so
     from foundationstereo_amd import update as fupdate
     fupdate.CONV_ENGINE = a.conv_engine
 
-    rank, local, world = fdist.init_from_env("nccl")
+    rank, local, world = fdist.init_from_env("nccl", force=a.dist)
+    wsz, backend = _world_info(world)
+    if wsz != a.gpus:
+        raise SystemExit(f"bench.py: rank {rank} sees world size {wsz} but --gpus {a.gpus}")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     torch.backends.cudnn.benchmark = bool(a.cudnn_benchmark)
@@ -228,23 +310,24 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the timed replays' range flag, read before anything else runs: the eager timing pass below
+    # goes through ops.guarded, which resets the flag.  A replay that overflowed also NaN-fills its
+    # output (the captured forward's last node, ops.range_poison_); both are reported
+    range_overflow = ops.range_overflowed(reset=False)
+    out_finite = bool(torch.isfinite(out).all())
     lk_step_ms, lk_step_n = ops.timer_query_clock("lookup") if a.graph else (0.0, 0)
     if a.graph:
         # graph replays carry no per-kernel events (HIP rejects external event nodes during
         # capture): time the kernels over one eager pass of the identical step instead, on one
         # stream -- with the side-stream overlap on, a kernel's event span would include the
         # time it shares the chip with another stream's kernels
-        # the lookup runs standalone in this pass (the timed step fuses it into convc1's staging,
-        # ops.conv1x1_lookup), so the roofline kernel of SURVEY §8d is the one measured
         overlap, fupdate.OVERLAP = fupdate.OVERLAP, False
-        fused, fupdate.FUSE_LOOKUP = fupdate.FUSE_LOOKUP, False
         ops.timer_enable(True)
         ops.timer_reset()
         runner._graph, saved = None, runner._graph
         step()
         runner._graph = saved
         fupdate.OVERLAP = overlap
-        fupdate.FUSE_LOOKUP = fused
     lk_ms, lk_n = ops.timer_query("lookup")
     cb_ms, cb_n = ops.timer_query("comb")
     cv_ms, cv_n = ops.timer_query("conv2d")
@@ -254,8 +337,7 @@ def main():
     lk_ck_ms, lk_ck_n = ops.timer_query_clock("lookup")
     cb_ck_ms, cb_ck_n = ops.timer_query_clock("comb")
     cv_flops = ops.conv_flops()
-    assert torch.isfinite(out).all()
-    range_overflow = ops.range_overflowed(reset=True)   # sticky over every forward of this run
+    range_overflow_eager = ops.range_overflowed(reset=True)   # the timing pass after the timed region
     # roofline durations, each the live measurement that agrees with rocprof's per-launch average
     # (profiles/*kernel_stats.csv): a single event-bracketed launch also holds ~5 us of
     # event-record latency (`avg_us_events`, kept for reference).
@@ -278,6 +360,8 @@ def main():
     lk_bytes = sum(lookup_bytes(bl, ph // 4, pw // 4, 28, L, args.corr_radius) for ph, pw in sizes) / len(sizes)
     cb_bytes = build_bytes(bl, C, sizes[-1][0] // 4, sizes[-1][1] // 4, D4)   # the replayed (last) launch
     lk_avg = lk_rep / 1e3 if lk_rep else (lk_ms / 1e3) / max(lk_n, 1)
+    lk_head_in_step = bool(lk_in_step)
+    lk_head = lk_in_step / 1e3 if lk_in_step else lk_avg          # seconds per launch, headline
     cb_avg = cb_rep / 1e3 if cb_rep else (cb_ms / 1e3) / max(cb_n, 1)
     traffic = traffic_build = None
     pmc_path = os.path.join(REPO, "profiles", f"pmc_lookup_summary_{a.config}.json")
@@ -297,6 +381,8 @@ def main():
         "value": pairs / elapsed,
         "unit": "pairs/s",
         "n_gpus": world,
+        "world_size": wsz,            # torch.distributed's view (1 without a process group)
+        "backend": backend,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": 1e3 * elapsed / a.steps,
@@ -311,7 +397,9 @@ def main():
                   else "f32 (3xfp16 split MFMA)"),
         "precision": a.precision,
         "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
-        "range_overflow": range_overflow,
+        "range_overflow": range_overflow,             # set during the timed replays
+        "range_overflow_timing_pass": range_overflow_eager,
+        "output_finite": out_finite,
         # forwards re-run in safe range mode after their range flag came back set (ops.guarded)
         "range_recoveries": ops.RANGE_RECOVERIES[0],
         "config": {"workload": f"{a.config}: {W}x{H}{' hierarchical' if a.config in HIERA else ''}, "
@@ -320,21 +408,22 @@ def main():
                    "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,
                    "corr_levels": L, "conv_engine": a.conv_engine, "hip_graph": bool(a.graph),
                    "parallelism": f"dp{world}"},
+        # headline: the lookup as it runs INSIDE the timed step (its in-kernel clock, first wave start
+        # to last wave end, baked into the captured graph: the last timed replay's launches, beside the
+        # other streams' kernels that share the chip and its HBM); the single-stream eager pass after
+        # the timed region is kept as a secondary figure
         "roofline": {"kernel": "geo_lookup", "bound": "hbm",
-                     "timed_over": ("single-stream eager step after the timed region" if a.graph else "timed region")
-                     + ("; standalone geo_lookup there, fused into convc1's staging in the timed step"
-                        if fupdate.FUSE_LOOKUP else ""),
-                     "achieved": lk_bytes / lk_avg / 1e9,
-                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_avg / HBM_PEAK,
-                     "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_avg * 1e6,
-                     "timed_by": "in-kernel clock over the eager step's launches" if lk_rep else "hip events",
-                     # the same kernel clock baked into the captured graph: the timed region's last replay,
-                     # the lookup beside the other streams' convs (they share the chip and its HBM)
-                     "avg_us_in_step": lk_in_step * 1e3 if lk_in_step else None,
-                     "frac_in_step": lk_bytes / (lk_in_step / 1e3) / HBM_PEAK if lk_in_step else None,
+                     "timed_over": ("the timed step (last replay's launches)" if lk_head_in_step else
+                                    "single-stream eager step after the timed region" if a.graph else "timed region"),
+                     "achieved": lk_bytes / lk_head / 1e9,
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": lk_bytes / lk_head / HBM_PEAK,
+                     "traffic": traffic, "algorithmic_bytes": lk_bytes, "avg_us": lk_head * 1e6,
+                     "timed_by": "in-kernel clock (s_memrealtime per wave) in the captured graph" if lk_head_in_step
+                                 else "in-kernel clock over the eager step's launches" if lk_rep else "hip events",
                      "launches_in_step": lk_step_n,
-                     "avg_us_events": lk_ev_ms * 1e3 / max(lk_n, 1),
-                     "avg_us_kernel_clock": lk_ck_ms * 1e3 / max(lk_ck_n, 1), "launches": lk_n},
+                     "avg_us_single_stream": lk_avg * 1e6,
+                     "frac_single_stream": lk_bytes / lk_avg / HBM_PEAK,
+                     "avg_us_events_single_stream": lk_ev_ms * 1e3 / max(lk_n, 1), "launches_single_stream": lk_n},
         # the refinement-loop convs (halo-tiled 3 x fp16 MFMA, split-K reduce included) hold most of
         # the step time; algorithmic = fp32 conv FLOPs, peak = dense fp16 MFMA / 3 products per MAC
         "roofline_conv": {"kernel": "conv*_halo_x3 (all halo convs: loop, 3D filter, context net)", "bound": "mfma",
@@ -374,7 +463,9 @@ def main():
                                "stages_s": {k: round(v, 3) for k, v in stages.items()}}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if not out_finite:
+        raise SystemExit("bench.py: the timed step returned non-finite disparities (range overflow)")
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

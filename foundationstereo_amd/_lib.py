@@ -28,8 +28,6 @@ SIGNATURES = {
     "fsmi_allpairs_corr": [_P, _P, _PP, _I, _I, _I, _I, _I, _P, _P],
     "fsmi_volume_pyramid": [_P, _PP, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_geo_lookup": [_PP, _PP, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
-    "fsmi_conv1x1_lookup": [_PP, _PP, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P,
-                            ctypes.c_longlong, _P],
     "fsmi_bilinear_sampler_1d": [_P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_disparity_regression": [_P, _P, _I, _I, _I, _I, _P],
     "fsmi_softmax_regression": [_P, _P, _I, _I, _I, _I, _P],
@@ -38,10 +36,6 @@ SIGNATURES = {
     "fsmi_gru_reset": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_gru_blend": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_conv3d_direct": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
-    "fsmi_conv2d": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I,
-                    _I, _I, _I, _I, _F, _I, _P],
-    "fsmi_conv2d_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _I, _P, _P, _P, _I, _P, _I, _I,
-                       _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
     "fsmi_conv2d_halo_x3": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _P, _P, _P, _I, _P, _I,
                             _I, _I, _I, _I, _I, _I, _I, _F, _I, _I, _P, ctypes.c_longlong, _P],
     "fsmi_conv2d_halo_x3_gate": [_PP, ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _P, _P, _P, _I, _P, _P, _P,
@@ -107,7 +101,7 @@ def load():
     if not os.path.exists(path):
         raise FsmiError(f"{os.path.basename(path)} not found at {path}: the HIP hot path is not built "
                         "(run `python -m foundationstereo_amd.build`, or __graft_entry__.build())")
-    lib = ctypes.CDLL(path)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None and name.startswith("fsmi_debug_"):   # debug hooks absent from an older A/B build

@@ -74,7 +74,9 @@ def build_library(force: bool = False, verbose: bool = False, defines=(), varian
         with ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
             list(ex.map(run, jobs))
     if force or jobs or _stale(lib, objs):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib])
+        # one SONAME for every build of the ABI: fsmi_torch.so's DT_NEEDED "libfsmi.so" then resolves to
+        # whichever build _lib.load() mapped first (e.g. libfsmi_fast.so), never to a second copy
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-soname,libfsmi.so", *objs, "-o", lib])
     return lib
 
 

@@ -54,6 +54,10 @@ bool take(int k, hipEvent_t* s, hipEvent_t* e) {
 constexpr size_t kClockArena = size_t(1) << 22;       // u64 stamps (32 MB)
 unsigned long long* g_clock = nullptr;
 size_t g_clock_top = 0;
+// slots handed to launches captured into a hipGraph (timer mode 2) stay reserved for the life of the
+// process: the graph keeps writing them on every replay, so a later session (clock_init) must never
+// hand the same addresses to new launches.  Sessions bump-allocate above this floor.
+size_t g_clock_floor = 0;
 std::vector<std::pair<size_t, long long>> g_clock_launch[FSMI_K_COUNT];
 
 static int clock_init() {
@@ -61,8 +65,10 @@ static int clock_init() {
     g_clock = nullptr;
     return FSMI_ERR_ARG;
   }
-  if (hipMemset(g_clock, 0, sizeof(unsigned long long) * kClockArena) != hipSuccess) return FSMI_ERR_ARG;
-  g_clock_top = 0;
+  if (hipMemset(g_clock + g_clock_floor, 0, sizeof(unsigned long long) * (kClockArena - g_clock_floor)) !=
+      hipSuccess)
+    return FSMI_ERR_ARG;
+  g_clock_top = g_clock_floor;
   for (auto& v : g_clock_launch) v.clear();
   return FSMI_OK;
 }
@@ -80,6 +86,7 @@ unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves)
   g_clock_launch[kernel].emplace_back(g_clock_top, nwaves);
   unsigned long long* p = g_clock + g_clock_top;
   g_clock_top += need;
+  if (st != hipStreamCaptureStatusNone) g_clock_floor = g_clock_top;   // baked into a graph: reserved
   return p;
 }
 

@@ -32,15 +32,25 @@ def env_world() -> Tuple[int, int, int]:
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
-def init_from_env(backend: str = "nccl") -> Tuple[int, int, int]:
+def init_from_env(backend: str = "nccl", force: bool = False) -> Tuple[int, int, int]:
+    """Join the torchrun process group (world > 1).  ``force``: create the group even for a single
+    process (rank 0 of 1, on 127.0.0.1), so that a one-GPU run moves its batch and results through
+    the same collectives as a multi-GPU one (RCCL with ``backend`` "nccl")."""
     rank, local, world = env_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+            s.close()
+        kw = dict(rank=rank, world_size=world)
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, device_id=torch.device("cuda", local), **kw)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **kw)
     return rank, local, world
 
 
@@ -113,7 +123,7 @@ class ShardedStereo:
     def _scatter(self, batch):
         """rank 0's batch -> every rank's local buffer (no collective at world 1)."""
         local = self._local_buffer(batch)
-        if not (self.world > 1 and dist.is_initialized()):
+        if not dist.is_initialized():            # a process group of one still runs the collectives
             local.copy_(batch)
             return local
         host = _host_staged()
@@ -175,7 +185,7 @@ class ShardedStereo:
             raise ValueError(f"batch {B} not divisible by world size {self.world}")
         local = self._scatter(batch)
         disp = self._run(local)
-        if not (self.world > 1 and dist.is_initialized()):
+        if not dist.is_initialized():
             return disp
         if _host_staged():
             parts = [torch.empty_like(disp, device="cpu") for _ in range(self.world)]

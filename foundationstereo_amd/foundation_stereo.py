@@ -191,6 +191,21 @@ class hourglass(nn.Module):
         return hit[1], hit[2]
 
 
+def _poison_outputs(out):
+    """ops.range_poison_ on every tensor of a captured forward's result (a tensor, or the
+    (init_disp, disp_preds) pair of training mode); a non-contiguous one is replaced by a contiguous
+    copy first, so the poison reaches every element the caller reads."""
+    if isinstance(out, torch.Tensor):
+        if not out.is_floating_point():
+            return out
+        if not out.is_contiguous():
+            out = out.contiguous()
+        return ops.range_poison_(out)
+    if isinstance(out, (list, tuple)):
+        return type(out)(_poison_outputs(o) for o in out)
+    return out
+
+
 class FoundationStereo(nn.Module):
     """core/foundation_stereo.py:127-274 (minus the out-of-scope backbone)."""
 
@@ -287,9 +302,13 @@ class FoundationStereo(nn.Module):
     def forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):
         """core/foundation_stereo.py:194-254.  On a HIP device outside graph capture the range guard
         of the split-precision convs is enforced here, once per forward: the flag is read after the
-        forward (one synchronisation) and a forward that overflowed is re-run in safe range mode
-        (ops.guarded) -- no disparity computed past the flag is returned.  A captured forward ends
-        with a device-side check instead (ops.range_poison_: NaN on overflow)."""
+        forward and a forward that overflowed is re-run in safe range mode (ops.guarded) -- no
+        disparity computed past the flag is returned.  That read synchronises the host with the
+        device once per eager forward; a caller that checks ``ops.check_range()`` itself can set
+        ``foundation_stereo.RANGE_GUARD = False`` to skip it.  A captured forward ends with a
+        device-side check instead: every returned disparity tensor (test mode's one, or
+        ``init_disp`` and each of ``disp_preds``) is NaN-filled when the flag is set
+        (ops.range_poison_)."""
         def run():
             return self._forward(image1, image2, iters, flow_init, test_mode, low_memory, init_disp)
         if not (image1.is_cuda and RANGE_GUARD):
@@ -298,10 +317,7 @@ class FoundationStereo(nn.Module):
             # a captured forward cannot synchronise: its last node NaN-fills the disparity when the
             # flag is set, so a replay that overflowed never returns a finite result (ShardedStereo
             # reads the flag after a replay and recovers)
-            out = run()
-            if isinstance(out, torch.Tensor) and out.is_contiguous():
-                ops.range_poison_(out)
-            return out
+            return _poison_outputs(run())
         return ops.guarded(run)
 
     def _forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):

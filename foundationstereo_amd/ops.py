@@ -265,31 +265,18 @@ def conv3d_direct(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
-def pack_conv_weight(*weights: Tensor) -> Tensor:
-    """Pack conv weights (Cout_i, Cin, KH, KW), stacked along Cout, into the
-    ``fsmi_conv2d`` layout [KH*KW*Cin][roundup(Cout,4)] (k = (kh*KW + kw)*Cin + ci)."""
-    w = torch.cat([x.detach().float() for x in weights], 0)
-    Cout, Cin, KH, KW = w.shape
-    coutp = (Cout + 3) // 4 * 4
-    pk = torch.zeros((KH * KW * Cin, coutp), device=w.device, dtype=torch.float32)
-    pk[:, :Cout] = w.permute(2, 3, 1, 0).reshape(KH * KW * Cin, Cout)
-    return pk
-
-
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "leaky": 6}   # leaky: halo kernel only
 
 
 class PackedConv:
-    """Conv weights packed once for the implicit-GEMM kernels.
-
-    ``mode`` "f32": fp32 MFMA (``fsmi_conv2d``); "x3": split-precision fp16
-    MFMA (``fsmi_conv2d_x3``: hi/lo halves of the weights pre-scaled by 2^wexp);
-    "halo": the same packed halves run by the halo-tiled ``fsmi_conv2d_halo_x3``
-    (square 1x1 / 3x3 only).
+    """Conv weights packed once for the halo-tiled split-precision kernels
+    (``fsmi_conv2d_halo_x3`` / ``fsmi_conv3d_halo_x3_ex``): fp16 hi / lo halves of each output
+    channel's weights pre-scaled by 2^wexp[co] (square 1x1 / 2x2 / 3x3 taps, optionally KD deep).
     Several weight tensors stacked along Cout form one conv (e.g. convz|convr).
     """
 
-    def __init__(self, *weights: Tensor, mode: str = "x3"):
+    def __init__(self, *weights: Tensor, mode: str = "halo"):
+        assert mode == "halo", f"PackedConv: mode {mode!r} (only the halo kernels remain)"
         w = torch.cat([x.detach().float() for x in weights], 0)
         if w.dim() == 5:                    # Conv3d (Cout, Cin, KD, KS, KS): taps kd-major
             self.kd = w.shape[2]
@@ -300,28 +287,17 @@ class PackedConv:
         self.cout, self.cin, self.k, kw, _ = w.shape
         assert self.k == kw
         self.mode = mode
-        assert mode in ("f32", "x3", "halo"), mode
-        assert mode != "halo" or self.k in (1, 2, 3), "halo conv: 1x1, 2x2 (transposed-conv phases) or 3x3"
-        assert self.kd == 1 or mode == "halo", "3D weights: halo mode only"
-        if mode == "f32":
-            self.wpk = pack_conv_weight(w[..., 0])
-            return
-        import math
-        amax = float(w.abs().max())
-        self.wexp = 0 if amax == 0 else -int(math.floor(math.log2(amax)))   # max |w| * 2^wexp in [1, 2)
+        assert self.k in (1, 2, 3), "halo conv: 1x1, 2x2 (transposed-conv phases) or 3x3"
         cinp = (self.cin + 31) // 32 * 32
         coutp = (self.cout + 31) // 32 * 32
-        if mode == "halo":
-            # per output channel: row max |w| * 2^e[co] in [1, 2) -- BN folding spreads the rows'
-            # scales over decades, and a per-tensor exponent would leave the small rows' lo halves
-            # fp16-subnormal (~11-bit weights).  The kernel multiplies row co by wscale[co] = 2^-e[co].
-            rmax = w.abs().reshape(self.cout, -1).amax(1).double()
-            e = torch.where(rmax > 0, -torch.floor(torch.log2(torch.where(rmax > 0, rmax, torch.ones_like(rmax)))),
-                            torch.zeros_like(rmax)).clamp(-100, 100)
-            row_scale = torch.pow(2.0, e).float().view(-1, 1, 1, 1, 1)
-            self.wscale = torch.pow(2.0, -e).float().contiguous()
-        else:
-            row_scale = 2.0 ** self.wexp
+        # per output channel: row max |w| * 2^e[co] in [1, 2) -- BN folding spreads the rows'
+        # scales over decades, and a per-tensor exponent would leave the small rows' lo halves
+        # fp16-subnormal (~11-bit weights).  The kernel multiplies row co by wscale[co] = 2^-e[co].
+        rmax = w.abs().reshape(self.cout, -1).amax(1).double()
+        e = torch.where(rmax > 0, -torch.floor(torch.log2(torch.where(rmax > 0, rmax, torch.ones_like(rmax)))),
+                        torch.zeros_like(rmax)).clamp(-100, 100)
+        row_scale = torch.pow(2.0, e).float().view(-1, 1, 1, 1, 1)
+        self.wscale = torch.pow(2.0, -e).float().contiguous()
         ws = torch.zeros((coutp, cinp, self.kd, self.k, self.k), device=w.device, dtype=torch.float32)
         ws[:self.cout, :self.cin] = w.permute(0, 1, 4, 2, 3) * row_scale
         # [tap = (kd, kh, kw)][cin chunk][cout][32]
@@ -333,20 +309,33 @@ class PackedConv:
         self._sb = {}
 
     def scale_bias(self, bias: Tensor = None) -> Tensor:
-        """(2^-wexp[co], bias[co]) pairs, 2*Cout floats, for the halo kernels' epilogue (cached
-        per bias tensor and version, so a captured graph keeps reading one stable buffer)."""
+        """(2^-wexp[co], bias[co]) pairs, 2*Cout floats, for the halo kernels' epilogue, cached per
+        bias tensor and version so that a captured graph keeps reading one stable buffer.
+
+        Entries for parameters (and for biases first seen during a stream capture, whose buffer a
+        graph node now holds) live as long as this PackedConv.  A per-call temporary bias (e.g.
+        ``bias.float()`` under a half model) keeps only its latest entry: an entry is valid only for
+        the very tensor object it was built from (a weak reference, so a recycled address is never
+        a false hit), and each eager use records the current stream on the buffer, so dropping it
+        later cannot hand its memory to a new allocation while a kernel on another stream may still
+        read it."""
+        import weakref
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         key = None if bias is None else (bias.data_ptr(), bias._version)
         hit = self._sb.get(key)
+        if hit is not None and hit[1] is not None and hit[1]() is not bias:
+            hit = None                   # the address now belongs to another tensor
         if hit is None:
             b = torch.zeros_like(self.wscale) if bias is None else bias.detach().float().reshape(-1)
             assert b.numel() == self.cout, f"bias of {b.numel()} for {self.cout} output channels"
-            if bias is not None and not isinstance(bias, torch.nn.Parameter):
-                # a per-call temporary (e.g. bias.float() under a half model): keep only the latest
-                # such entry so the cache stays bounded; parameters are bounded by the module tree
-                for k in [k for k, v in self._sb.items() if v[1] is not None
-                          and not isinstance(v[1], torch.nn.Parameter)]:
+            pinned = bias is None or isinstance(bias, torch.nn.Parameter) or capturing
+            if not pinned:
+                for k in [k for k, v in self._sb.items() if not v[2]]:
                     del self._sb[k]
-            hit = self._sb[key] = (torch.stack([self.wscale, b], 1).contiguous(), bias)
+            hit = self._sb[key] = (torch.stack([self.wscale, b], 1).contiguous(),
+                                   None if bias is None else weakref.ref(bias), pinned)
+        if not hit[2] and not capturing and hit[0].is_cuda:
+            hit[0].record_stream(torch.cuda.current_stream(hit[0].device))
         return hit[0]
 
 
@@ -504,66 +493,6 @@ def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Te
     del keep
 
 
-def lookup_channel_order(L: int, Cv: int, radius: int = 4) -> Tensor:
-    """Input-channel order of ``fsmi_conv1x1_lookup``: the index, in the lookup's channel layout
-    (core/geometry.py:62-65: per level [geo c*K + k ..., corr k ...], K = 2r+1), of each kernel
-    channel (-1: a zero row).  Chunk q of 32 holds groups 3q..3q+2 (group = level*(Cv+1) + c)."""
-    K = 2 * radius + 1
-    gpc = 32 // K
-    G = L * (Cv + 1)
-    nck = (G + gpc - 1) // gpc
-    order = torch.full((nck * 32,), -1, dtype=torch.long)
-    for g in range(G):
-        i, c = divmod(g, Cv + 1)
-        for k in range(K):
-            order[(g // gpc) * 32 + (g % gpc) * K + k] = i * K * (Cv + 1) + c * K + k
-    return order
-
-
-def pack_lookup_conv(weight: Tensor, L: int, Cv: int, radius: int = 4) -> "PackedConv":
-    """convc1's (Cout, L*K*(Cv+1), 1, 1) weight re-ordered for ``fsmi_conv1x1_lookup`` and packed."""
-    order = lookup_channel_order(L, Cv, radius).to(weight.device)
-    w = weight.detach().float().reshape(weight.shape[0], -1)
-    assert w.shape[1] == L * (2 * radius + 1) * (Cv + 1), "pack_lookup_conv: channel count"
-    wn = torch.zeros(w.shape[0], order.numel(), device=w.device, dtype=w.dtype)
-    m = order >= 0
-    wn[:, m] = w[:, order[m]]
-    return PackedConv(wn.reshape(w.shape[0], -1, 1, 1), mode="halo")
-
-
-def conv1x1_lookup(vol_levels: Sequence[Tensor], corr_levels: Sequence[Tensor], disp: Tensor, radius: int,
-                   pk: "PackedConv", bias: Tensor = None, act=None, out: Tensor = None, co0: int = 0,
-                   nsplit: int = 2) -> Tensor:
-    """act(conv1x1(geo_lookup(vol_levels, corr_levels, disp, radius)) + bias) without the lookup
-    tensor (``fsmi_conv1x1_lookup``); ``pk`` from ``pack_lookup_conv``."""
-    _check("conv1x1_lookup", disp, *vol_levels, *corr_levels)
-    L = len(vol_levels)
-    B, Cv, D, H, W = vol_levels[0].shape
-    W2 = corr_levels[0].shape[-1]
-    assert disp.shape == (B, 1, H, W), f"disp {tuple(disp.shape)} vs volume {(B, 1, H, W)}"
-    for i in range(L):
-        assert vol_levels[i].shape == (B, Cv, D >> i, H, W) and vol_levels[i].is_contiguous()
-        assert corr_levels[i].shape == (B, H, W, W2 >> i) and corr_levels[i].is_contiguous()
-    K = 2 * radius + 1
-    assert pk.mode == "halo" and pk.k == 1 and pk.cin == lookup_channel_order(L, Cv, radius).numel(), \
-        "conv1x1_lookup: weights must come from pack_lookup_conv"
-    disp = _c(disp)
-    if out is None:
-        out = torch.empty((B, pk.cout, H, W), device=disp.device, dtype=torch.float32)
-    assert out.is_contiguous() and out.shape[0] == B and out.shape[2:] == (H, W)
-    if _CONV_FLOPS["on"]:
-        _CONV_FLOPS["flops"] += 2 * L * K * (Cv + 1) * pk.cout * B * H * W
-    stream = _stream(disp)
-    ws = _split_workspace(disp.device, stream, 8 * B * pk.cout * H * W)
-    pv, kv = _lib.ptr_array([_p(t) for t in vol_levels])
-    pc, kc = _lib.ptr_array([_p(t) for t in corr_levels])
-    _lib.check(_lib.load().fsmi_conv1x1_lookup(
-        pv, pc, _p(disp), L, radius, B, Cv, D, H, W, W2, _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
-        _p(out), out.shape[1], co0, pk.cout, ACT[act], nsplit, _p(ws), ws.numel(), stream), "conv1x1_lookup")
-    del kv, kc
-    return out
-
-
 # ---- measured tile / split-K choices per conv shape (tools/tune_conv.py -> tuning/fsmi_conv.json):
 # consulted when a caller leaves cfg / nsplit on auto; shapes not in the table use the C-side policy
 _TUNE_PATH = os.environ.get("FSMI_TUNE_PATH") or os.path.join(
@@ -627,51 +556,37 @@ def _split_workspace(dev, stream, floats: int):
     return ws
 
 
-def conv2d(segs, pk, cout: int = None, k: int = None, bias: Tensor = None, act=None, alpha: float = 1.0,
-           gamma: Tensor = None, res: Tensor = None, out: Tensor = None, co0: int = 0, cfg: int = -1,
-           nsplit: int = -1) -> Tensor:
-    """Implicit-GEMM conv (stride 1, 'same' zero padding) on MFMA.
+def conv2d(segs, pk, bias: Tensor = None, act=None, alpha: float = 1.0, gamma: Tensor = None,
+           res: Tensor = None, out: Tensor = None, co0: int = 0, cfg: int = -1, nsplit: int = -1) -> Tensor:
+    """Halo-tiled split-precision conv (stride 1, 'same' zero padding, ``fsmi_conv2d_halo_x3``).
 
     ``segs``: list of NCHW tensors or ``(tensor, c_start, c_count)`` channel slices,
-    concatenated along C without a copy.  ``pk``: a ``PackedConv`` (or a raw
-    ``pack_conv_weight`` tensor with ``cout``/``k`` given: fp32 path).  Writes
+    concatenated along C without a copy.  ``pk``: a ``PackedConv``.  Writes
     ``out[:, co0:co0+cout]`` (allocated as (B, cout, H, W) when None) =
     ``res + gamma * alpha * act(conv + bias)``."""
-    if isinstance(pk, torch.Tensor):
-        raw = pk
-        pk = PackedConv.__new__(PackedConv)
-        pk.mode, pk.wpk, pk.cout, pk.k = "f32", raw, cout, k
-        pk.cin = raw.shape[0] // (k * k)
     norm, (pp, chs, tots, keep), cin = _segments(segs)
     t0 = norm[0][0]
     B, _, H, W = t0.shape
     extra = [x for x in (bias, gamma, res) if x is not None]
     _check("conv2d", *[t for t, _, _ in norm], *extra)
-    assert cin == pk.cin, f"conv2d: {cin} input channels for a conv packed with {pk.cin}"
+    assert pk.mode == "halo" and cin == pk.cin, f"conv2d: {cin} input channels for a conv packed with {pk.cin}"
     if out is None:
         out = torch.empty((B, pk.cout, H, W), device=t0.device, dtype=torch.float32)
     assert out.is_contiguous() and out.shape[0] == B and out.shape[2:] == (H, W)
     if res is not None:
         assert res.is_contiguous() and res.shape[2:] == (H, W)
-    common = (_p(bias) if bias is not None else None, _p(gamma) if gamma is not None else None,
-              _p(res) if res is not None else None, res.shape[1] if res is not None else 0,
-              _p(out), out.shape[1], co0, B, pk.cout, pk.k, pk.k, H, W, ACT[act], float(alpha), cfg, _stream(t0))
-    lib = _lib.load()
     if _CONV_FLOPS["on"]:
         _CONV_FLOPS["flops"] += 2 * cin * pk.cout * pk.k * pk.k * B * H * W
-    if pk.mode == "f32":
-        _lib.check(lib.fsmi_conv2d(pp, chs, tots, len(norm), _p(pk.wpk), *common), "conv2d")
-    elif pk.mode == "x3":
-        _lib.check(lib.fsmi_conv2d_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), pk.wexp, *common),
-                   "conv2d_x3")
-    else:
-        # auto split-K is capped at 8; the workspace covers that for this output
-        ws = _split_workspace(t0.device, common[-1], 8 * B * pk.cout * H * W)
-        tcfg, nsplit = _tuned(pk.k, 1, cin, pk.cout, B, 1, H, W, cfg, nsplit)
-        hc = common[1:9] + (pk.k,) + common[11:-2] + (tcfg, nsplit, _p(ws), ws.numel(), common[-1])
-        _lib.check(lib.fsmi_conv2d_halo_x3(pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo),
-                                           _p(pk.scale_bias(bias)), *hc), "conv2d_halo_x3")
-        _range_debug(f"conv2d k{pk.k} {cin}->{pk.cout}", norm)
+    stream = _stream(t0)
+    # auto split-K is capped at 8; the workspace covers that for this output
+    ws = _split_workspace(t0.device, stream, 8 * B * pk.cout * H * W)
+    tcfg, nsplit = _tuned(pk.k, 1, cin, pk.cout, B, 1, H, W, cfg, nsplit)
+    _lib.check(_lib.load().fsmi_conv2d_halo_x3(
+        pp, chs, tots, len(norm), _p(pk.whi), _p(pk.wlo), _p(pk.scale_bias(bias)),
+        _p(gamma) if gamma is not None else None, _p(res) if res is not None else None,
+        res.shape[1] if res is not None else 0, _p(out), out.shape[1], co0, B, pk.cout, pk.k, H, W, ACT[act],
+        float(alpha), tcfg, nsplit, _p(ws), ws.numel(), stream), "conv2d_halo_x3")
+    _range_debug(f"conv2d k{pk.k} {cin}->{pk.cout}", norm)
     del keep
     return out
 

@@ -90,6 +90,12 @@ def load() -> None:
     if not os.path.exists(LIB):
         raise RuntimeError(f"{LIB} missing")
     if not _registered():                # a second TORCH_LIBRARY(fsmi) registration aborts
+        # map the runtime this process selected (libfsmi.so, or libfsmi_fast.so under
+        # FSMI_PRECISION=fast) first: every build carries the SONAME libfsmi.so, so the loader
+        # satisfies fsmi_torch.so's dependency with it instead of mapping a second runtime with its
+        # own timers, range flag and safe-mode switch
+        from . import _lib
+        _lib.load()
         torch.ops.load_library(EXT)
     _loaded = True
 

@@ -39,11 +39,6 @@ PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 
 # the disparity head writes disp + delta into the next encoder buffer (A/B knob)
 HEAD_INPLACE = os.environ.get("FSMI_HEAD_INPLACE", "1") != "0"
-# opt-in (A/B): the lookup fused into convc1's staging (ops.conv1x1_lookup), so the lookup tensor
-# never exists.  Parity-green but measured slower end to end (cfg2: 15.8 vs 16.6 pairs/s; the fused
-# kernel 279 us vs 169 us for lookup + convc1 alone): its gathers sit on the conv's critical path at
-# one wave per SIMD (276 VGPRs), where the standalone lookup hides them across 4x more waves
-FUSE_LOOKUP = os.environ.get("FSMI_FUSE_LOOKUP", "0") == "1"
 _CONVD1_MIOPEN = os.environ.get("FSMI_CONVD1_MIOPEN", "0") == "1"
 _POOL_TORCH = os.environ.get("FSMI_POOL_TORCH", "0") == "1"        # A/B knob: torch avg_pool2d
 
@@ -177,31 +172,8 @@ class BasicMotionEncoder(nn.Module):
         """Writes cat([relu(conv(...)), disp]) into ``out`` (B, 128, H, W) without the cat copy."""
         return self._encode_rest(disp, _conv(self.convc1, [corr], "relu"), out)
 
-    def encode_geo_into(self, disp, geo, out):
-        """``encode_into(disp, geo(disp), out)`` with the lookup fused into convc1's input staging
-        (``ops.conv1x1_lookup``): the (B, L*9*(Cv+1), H, W) lookup tensor is never written."""
-        L, Cv = geo.num_levels, geo.shape[1]
-        w, bias = self.convc1.weight, self.convc1.bias
-        key = (w.data_ptr(), w._version, L, Cv, geo.radius)
-        hit = self.__dict__.get("_fsmi_lookup_pack")
-        if hit is None or hit[0] != key:
-            with torch.no_grad():
-                hit = (key, ops.pack_lookup_conv(w, L, Cv, geo.radius))
-            self.__dict__["_fsmi_lookup_pack"] = hit
-        c1 = ops.conv1x1_lookup(geo.geo_volume_pyramid, geo.init_corr_pyramid, disp, geo.radius, hit[1],
-                                bias=_f32(bias), act="relu")
-        return self._encode_rest(disp, c1, out)
-
-    def fused_lookup_ok(self, geo) -> bool:
-        from .geometry import Combined_Geo_Encoding_Volume
-        return (FUSE_LOOKUP and isinstance(geo, Combined_Geo_Encoding_Volume) and geo.radius == 4
-                and self.convc1.out_channels <= 256
-                and self.convc1.in_channels == geo.num_levels * 9 * (geo.shape[1] + 1))
-
     def motion_into(self, disp, geo_fn, out):
         """The motion path of one iteration: the lookup ``geo_fn(disp)`` and this encoder."""
-        if self.fused_lookup_ok(geo_fn):
-            return self.encode_geo_into(disp, geo_fn, out)
         return self.encode_into(disp, geo_fn(disp), out)
 
     def _encode_rest(self, disp, c1, out):

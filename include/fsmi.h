@@ -95,20 +95,6 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
                     int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
                     void* stream);
 
-/* ---- a6 + a7: lookup fused into the motion encoder's convc1 ------------------
- * replaces core/update.py:62 F.relu(self.convc1(corr)) with corr = the lookup above
- * (core/geometry.py:43-65): out[b, co0+co] = act(bias[co] + sum_ch W[co, ch] lookup[b, ch])
- * without materialising the lookup.  Arguments of fsmi_geo_lookup (radius 4), then a
- * 1x1 conv in fsmi_conv2d_halo_x3's packing whose input channels follow the chunk
- * order of the kernel: chunk q = groups 3q..3q+2 (group g = level*(Cv+1) + c, c == Cv the
- * correlation group) as channels (g-3q)*9 + k, channels 27..31 zero
- * (ops.pack_lookup_conv).  Cout <= 256; act 0 none / 1 ReLU; nsplit split-K factor
- * (partials in ws, B*Cout*H*W floats each). */
-int fsmi_conv1x1_lookup(const float* const* vol_levels, const float* const* corr_levels, const float* disp,
-                        int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
-                        const void* whi, const void* wlo, const float* scale_bias, float* out, int out_ctot,
-                        int co0, int Cout, int act, int nsplit, float* ws, long long ws_floats, void* stream);
-
 /* 1-D stereo specialisation of bilinear_sampler (core/utils/utils.py:44-55):
  * img (P,C,1,Lx); x (P,K) pixel x-coordinates (y == 0); out (P,C,1,K). */
 int fsmi_bilinear_sampler_1d(const float* img, const float* x, float* out,
@@ -151,38 +137,20 @@ int fsmi_gru_blend(const float* zr_s, const float* zr_l, const float* q_s, const
 int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float* out,
                        int B, int Cin, int Cout, int KS, int D, int H, int W, void* stream);
 
-/* ---- a7: implicit-GEMM 2D convolution (fp32 MFMA) ------------------------
+/* Convolution of the refinement loop, halo-tiled split-precision MFMA.
  * replaces the nn.Conv2d / nn.Linear stacks of the refinement loop
  * (core/update.py:20-159: motion encoder, SelectiveConvGRU convs, DispHead,
  * mask head) plus the elementwise passes that follow them.
  * Input: nseg NCHW channel segments concatenated along C (zero-copy cat):
  *   segment i = seg_ch[i] channels starting at seg_ptr[i] inside a tensor with
  *   seg_ctot[i] channels per image (batch stride seg_ctot[i]*H*W).
- * wpk: weights packed [KH*KW*Cin][roundup(Cout,4)] (k = (kh*KW+kw)*Cin + ci), zero padded.
  * out[b, co0+co] (tensor with out_ctot channels) =
- *   res[b,co] + gamma[co] * alpha * act(conv + bias[co]);  act 0 none, 1 ReLU, 2 GELU(erf)
- *   (fsmi_conv2d_halo_x3 also 6: LeakyReLU 0.01);
- *   bias/gamma/res may be NULL (res has res_ctot channels per image).
- * KHxKW in {1x1, 3x3, 7x7}, stride 1, zero padding K/2.  cfg: tile config or -1 (auto). */
-int fsmi_conv2d(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
-                const float* wpk, const float* bias, const float* gamma, const float* res, int res_ctot,
-                float* out, int out_ctot, int co0, int B, int Cout, int KH, int KW, int H, int W, int act,
-                float alpha, int cfg, void* stream);
-
-/* Same convolution with split-precision operands on the fp16 MFMA ("3 x fp16"):
- * x = hi + lo (two fp16), product = hi*hi + hi*lo + lo*hi accumulated in fp32
- * (~22-bit operands, ~5x the fp32-MFMA rate).  whi/wlo: _Float16 weights packed
- * [KH*KW][Cin32/32][Cout32][32] (Cin32/Cout32 = Cin/Cout rounded up to 32, zero
- * padded), pre-multiplied by 2^wexp; the epilogue multiplies by 2^-wexp.  A/B and test
- * kernel (the product path runs fsmi_conv2d_halo_x3): one weight exponent per tensor and no
- * activation scaling, so it needs |x| < 65504 and keeps ~22 bits only for |x| >~ 0.1. */
-int fsmi_conv2d_x3(const float* const* seg_ptr, const int* seg_ch, const int* seg_ctot, int nseg,
-                   const void* whi, const void* wlo, int wexp, const float* bias, const float* gamma,
-                   const float* res, int res_ctot, float* out, int out_ctot, int co0, int B, int Cout,
-                   int KH, int KW, int H, int W, int act, float alpha, int cfg, void* stream);
-
-/* Halo-tiled variant of fsmi_conv2d_x3 (same packed layout, same epilogue) for
- * square KS in {1, 3}.  Range-safe split: each output channel's weights are packed
+ *   res[b,co] + gamma[co] * alpha * act(conv + bias[co]);  act 0 none, 1 ReLU, 2 GELU(erf),
+ *   6 LeakyReLU 0.01; gamma/res may be NULL (res has res_ctot channels per image).
+ * Split-precision operands on the fp16 MFMA ("3 x fp16"): x = hi + lo (two fp16),
+ * product = hi*hi + hi*lo + lo*hi accumulated in fp32 (~22-bit operands).  whi/wlo:
+ * _Float16 weights packed [KS*KS][Cin32/32][Cout32][32] (Cin32/Cout32 = Cin/Cout rounded
+ * up to 32, zero padded).  Square KS in {1, 3}.  Range-safe split: each output channel's weights are packed
  * x 2^wexp[co] (its max |w| in [1, 2)); scale_bias (2*Cout floats, device, 8-B
  * aligned) holds the pairs (2^-wexp[co], bias[co]) the epilogue applies as
  * conv * scale + bias; activations get a block exponent per 32-channel chunk in the
@@ -234,7 +202,7 @@ int fsmi_conv2d_halo_x3_gate(const float* const* seg_ptr, const int* seg_ch, con
  * halo split-precision kernel: a KD x KS x KS conv (KS in {1,3}, KD odd, zero
  * padding KD/2, KS/2) is the sum over kd of 2D convs on depth plane d+kd-KD/2.
  * x (B,Cin,D,H,W), out / res (B,Cout,D,H,W); whi/wlo packed as for
- * fsmi_conv2d_x3 with taps = (kd, kh, kw), kd major; bias = folded conv bias +
+ * fsmi_conv2d_halo_x3 with taps = (kd, kh, kw), kd major; bias = folded conv bias +
  * BatchNorm shift.  out = act(conv + bias) + res, or with res_pre
  * act(conv + bias + res); act 0 none, 1 ReLU, 6 LeakyReLU(0.01).
  * cfg as fsmi_conv2d_halo_x3 plus 6: 32 couts x 8x32 px, 7: 32 x 4x32. */

@@ -1,4 +1,4 @@
-"""The forward an UNMODIFIED reference ``FoundationStereo`` runs after ``patch_reference``.
+"""Test infrastructure (not product code): the forward an UNMODIFIED reference ``FoundationStereo`` runs after ``patch_reference``.
 
 ``patch_reference(core.foundation_stereo)`` rebinds the reference module's star-imported names to
 this package, but the reference's own ``forward`` / ``upsample_disp`` bodies stay
@@ -20,9 +20,9 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from .foundation_stereo import autocast, normalize_image
-from .geometry import Combined_Geo_Encoding_Volume
-from .submodule import build_concat_volume, build_gwc_volume, context_upsample, disparity_regression
+from foundationstereo_amd.foundation_stereo import autocast, normalize_image
+from foundationstereo_amd.geometry import Combined_Geo_Encoding_Volume
+from foundationstereo_amd.submodule import build_concat_volume, build_gwc_volume, context_upsample, disparity_regression
 
 
 def upsample_disp_reference_order(model, disp, mask_feat_4, stem_2x):

@@ -140,36 +140,6 @@ def test_conv3d_direct_vs_torch(ops_mod, KS, shape):
     close(ops_mod.conv3d_direct(g(x), g(w), g(b)), ref, atol=2e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("mode", ["f32", "x3"])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3])
-@pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (7, 64, "relu"), (3, 128, None)])
-def test_conv2d_mfma_vs_torch(ops_mod, mode, cfg, k, cout, act):
-    """Implicit-GEMM conv (fp32 MFMA and split-precision 3 x fp16 MFMA): 2 input segments (one a
-    channel slice), ragged pixels/couts, output slice, every epilogue term, all tile configs; vs an
-    fp64 torch reference.  Tolerance 2e-5 abs + 1e-5 rel for both (x3 operands carry 22 bits)."""
-    import torch.nn.functional as F
-    B, H, W = 2, 9, 13
-    a_ = synth.normal(91, (B, 5, H, W))
-    c_ = synth.normal(92, (B, 12, H, W))
-    cin = 5 + 7 if k != 7 else 1
-    w = synth.normal(93, (cout, cin, k, k), 0.2)
-    bias = synth.normal(94, (cout,), 0.1)
-    gamma = synth.uniform(95, (cout,), 0.5, 1.5)
-    res = synth.normal(96, (B, cout, H, W))
-    if k == 7:
-        segs, x = [g(a_[:, :1].copy())], t(a_[:, :1])
-    else:
-        segs, x = [g(a_), (g(c_), 3, 7)], torch.cat([t(a_), t(c_[:, 3:10])], 1)
-    out = torch.zeros(B, cout + 3, H, W, device=DEV)
-    ops_mod.conv2d(segs, ops_mod.PackedConv(g(w), mode=mode), bias=g(bias), act=act, alpha=0.75, gamma=g(gamma),
-                   res=g(res), out=out, co0=2, cfg=cfg)
-    y = F.conv2d(x.double(), t(w).double(), t(bias).double(), padding=k // 2)
-    y = {"relu": F.relu, "gelu": F.gelu, None: lambda v: v}[act](y)
-    ref = t(res).double() + t(gamma).double().view(1, -1, 1, 1) * 0.75 * y
-    close(out[:, 2:2 + cout], ref, atol=2e-5, rtol=1e-5)
-    assert float(out[:, :2].abs().max()) == 0 and float(out[:, 2 + cout:].abs().max()) == 0
-
-
 @pytest.mark.parametrize("HW", [(19, 45), (12, 40)])
 @pytest.mark.parametrize("nsplit", [1, 2])
 @pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 8, 9, 19, 20, 21, 23])
@@ -351,32 +321,6 @@ def test_hourglass_gated_vs_unfused(ops_mod):
         finally:
             sub.FATT_FUSE, sub.S2_3D = old
     close(a, b.double(), atol=5e-5, rtol=5e-5)
-
-
-@pytest.mark.parametrize("L,Cv,D,H,W,B,nsplit", [(4, 28, 48, 12, 40, 1, 1), (2, 8, 24, 5, 37, 2, 2),
-                                                   (4, 28, 48, 30, 40, 1, 3), (3, 28, 80, 7, 64, 1, 2)])
-def test_conv1x1_lookup_vs_unfused(ops_mod, L, Cv, D, H, W, B, nsplit):
-    """convc1 with the lookup fused into its staging (fsmi_conv1x1_lookup) vs geo_lookup + the halo
-    1x1 conv on the same inputs and weights: disparities below 0, beyond D and on integers, ragged
-    pixel tiles (H*W not a multiple of 64), batch 2, split-K; within the split-precision tolerance."""
-    import torch.nn.functional as F
-    r, K = 4, 9
-    gen = torch.Generator().manual_seed(31 + L + Cv)
-    vol = torch.randn(B, Cv, D, H, W, generator=gen).to(DEV)
-    fl, fr = (torch.randn(B, 32, H, W, generator=gen).to(DEV) for _ in range(2))
-    corr = ops_mod.allpairs_corr(fl, fr, L)
-    pyr = ops_mod.volume_pyramid(vol, L)
-    disp = (torch.rand(B, 1, H, W, generator=gen) * (D + 8) - 4).to(DEV)
-    disp[..., 0, :3] = torch.tensor([0.0, 5.0, float(D - 1)], device=DEV)
-    cin = L * K * (Cv + 1)
-    w = (torch.randn(256, cin, 1, 1, generator=gen) * 0.05).to(DEV)
-    bias = torch.randn(256, generator=gen).to(DEV)
-    lk = ops_mod.geo_lookup(pyr, corr, disp, r)
-    ref = F.relu(F.conv2d(lk.double(), w.double(), bias.double()))
-    out = ops_mod.conv1x1_lookup(pyr, corr, disp, r, ops_mod.pack_lookup_conv(w, L, Cv, r), bias=bias, act="relu",
-                                 nsplit=nsplit)
-    close(out, ref, atol=2e-5, rtol=1e-5)
-    assert not ops_mod.range_overflowed(reset=True)
 
 
 @pytest.mark.parametrize("scale", [3e5, 1e3, 1e-4, 1e-7])

@@ -55,7 +55,7 @@ def _product(args, H, W, shift, seed=1234):
 
 @pytest.mark.parametrize("name", ["e2e_tiny", "e2e_cfg1_L2", "e2e_cfg1_L4"])
 def test_reference_order_vs_golden(lib, name):
-    from foundationstereo_amd.reference_order import forward_reference_order
+    from tests.reference_order import forward_reference_order
     gd = load_golden(name)
     H, W, md, iters, L, shift = (int(v) for v in gd["meta"])
     args = synth.make_args(max_disp=md, corr_levels=L, vit_size="vits")
@@ -75,7 +75,7 @@ def test_reference_order_vs_golden(lib, name):
 
 def test_reference_order_train_mode_outputs(lib):
     """test_mode=False: (init_disp, one upsampled prediction per iteration), like the reference."""
-    from foundationstereo_amd.reference_order import forward_reference_order
+    from tests.reference_order import forward_reference_order
     gd = load_golden("e2e_tiny")
     H, W, md, iters, L, shift = (int(v) for v in gd["meta"])
     args = synth.make_args(max_disp=md, corr_levels=L, vit_size="vits")
@@ -89,7 +89,7 @@ def test_reference_order_train_mode_outputs(lib):
 @pytest.mark.timeout(600)
 def test_reference_order_vs_oracle_cfg2(lib):
     """The bench geometry (640x480, D192, L=4) at 2 iterations vs the CPU oracle."""
-    from foundationstereo_amd.reference_order import forward_reference_order
+    from tests.reference_order import forward_reference_order
     H, W, md, iters, L = 480, 640, 192, 2, 4
     args = synth.make_args(max_disp=md, corr_levels=L, vit_size="vits")
     m, (fl, fr, vf), (left, right) = _product(args, H, W, 8)

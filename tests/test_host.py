@@ -148,14 +148,3 @@ def test_conv_tuning_db_wellformed():
                 or (24 <= e["cfg"] <= 26 and ks == 1 and kd == 1 and D == 1)
                 or (e["cfg"] == 30 and kd == 17 and ks == 1)
                 or 34 <= e["cfg"] <= 41) and 1 <= e["nsplit"] <= 8, (key, e)
-
-
-def test_lookup_channel_order():
-    """fsmi_conv1x1_lookup's input-channel order: 3 whole (level, channel) groups of 9 taps per
-    32-channel chunk, every lookup channel exactly once, 5 zero rows per chunk."""
-    from foundationstereo_amd import ops
-    o = ops.lookup_channel_order(4, 28, 4)
-    assert o.numel() == 39 * 32 and sorted(o[o >= 0].tolist()) == list(range(4 * 9 * 29))
-    assert o[:27].tolist() == list(range(27)) and (o[27:32] == -1).all()
-    assert o[32:41].tolist() == list(range(27, 36))
-    assert o[9 * 32 + 9:9 * 32 + 18].tolist() == list(range(252, 261))   # group 28: level 0 corr

@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from foundationstereo_amd import ops, synth  # noqa: E402
-from foundationstereo_amd.reference_order import forward_reference_order  # noqa: E402
+from tests.reference_order import forward_reference_order  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="cfg2")
