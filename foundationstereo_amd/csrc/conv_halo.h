@@ -1368,6 +1368,10 @@ void launch_tile(const HaloArgs& a, hipStream_t s) {
       case 6: launch_tile<KS, 32, 8, 1, true, D3>(a, s); break;                             \
       case 8: launch_tile<KS, 128, 8, 2, true, D3>(a, s); break;                            \
       case 9: launch_tile<KS, 256, 4, 4, true, D3>(a, s); break;                            \
+      case 11:                                                                              \
+        if constexpr (!D3 && KS != 2) launch_tile<KS, 256, 5, 4, true, D3>(a, s);           \
+        else { set_error("fsmi_conv_halo: tile 11 is 2D only"); return FSMI_ERR_ARG; }      \
+        break;                                                                              \
       default: launch_tile<KS, 32, 4, 1, true, D3>(a, s); break;                            \
     }                                                                                       \
     return finish_launch("fsmi_conv_halo");                                                 \

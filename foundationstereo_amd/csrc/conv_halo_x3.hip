@@ -159,7 +159,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     // accumulator rescaling) with D = KD = 1 is the same 2D conv; the pointwise tiles (mode 2 only)
     // take the 128 x 2 x 32 register-weight tile
     d3 = true;
-    if (cfg >= 24) cfg = 4;
+    if (cfg == 11 || cfg == 43) cfg = 9;           // the 5-row tile is 2D only
+    else if (cfg >= 24 && cfg <= 26) cfg = 4;      // (pipelined 32 + c: the plain tile c, below)
   }
   if (cfg == 30) {                                 // depth-blocked (17, 1, 1) tile (conv_depth.hip)
     FSMI_CHECK_ARG(d3 && KS == 1 && KD == 17 && a.str == 1 && !a.up, "%s: tile 30 takes (17, 1, 1) stride-1 "
@@ -177,8 +178,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   // conv_halo_pipe_kernel); the volume instantiation (safe range mode) keeps the plain tile
   if (cfg >= 32) {
     cfg -= 32;
-    FSMI_CHECK_ARG(cfg >= 2 && cfg <= 9 && a.str == 1 && !a.up, "%s: pipelined tile 32 + %d (2..9, stride 1)", what,
-                   cfg);
+    FSMI_CHECK_ARG(((cfg >= 2 && cfg <= 9) || cfg == 11) && a.str == 1 && !a.up,
+                   "%s: pipelined tile 32 + %d (2..9, 11; stride 1)", what, cfg);
     a.pipe = d3 ? 0 : 1;
   }
   const bool pw = cfg >= 24;
@@ -195,8 +196,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     cfg -= 16;
     FSMI_CHECK_ARG(halo::kg2_tile(cfg), "%s: tile %d has no K-group variant (16 + 3/4/5/7)", what, cfg);
   }
-  FSMI_CHECK_ARG((cfg >= 0 && cfg <= 9) || pw || (a.str == 2 && cfg == 10), "%s: cfg %d (0..9, 16 + 3/4/5/7, 24..26)",
-                 what, cfg);
+  FSMI_CHECK_ARG((cfg >= 0 && cfg <= 9) || pw || (a.str == 2 && cfg == 10) || (cfg == 11 && !d3 && KS != 2),
+                 "%s: cfg %d (0..9, 11 on 2D maps, 16 + 3/4/5/7, 24..26)", what, cfg);
   FSMI_CHECK_ARG(a.str == 1 || (kg == 1 && (cfg == 4 || cfg == 5 || cfg == 7 || cfg == 10)),
                  "%s: stride-2 tile %d (4, 5, 7, 10)", what, cfg);
   if (pw) halo::pw_tile(cfg, a);
@@ -208,6 +209,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     case 6: tile_counts<3, 32, 8, 1>(a); break;
     case 8: tile_counts<3, 128, 8, 2>(a); break;
     case 9: tile_counts<3, 256, 4, 4>(a); break;
+    case 11: tile_counts<3, 256, 5, 4>(a); break;  // 5 rows: 24 row tiles at 120 (one round at 2 cout tiles)
     case 10: tile_counts<3, 64, 2, 2>(a); break;
     default: tile_counts<3, 32, 4, 1>(a); break;
   }

@@ -142,7 +142,7 @@ def test_conv3d_direct_vs_torch(ops_mod, KS, shape):
 
 @pytest.mark.parametrize("HW", [(19, 45), (12, 40)])
 @pytest.mark.parametrize("nsplit", [1, 2])
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 8, 9, 19, 20, 21, 23])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 8, 9, 11, 19, 20, 21, 23])
 @pytest.mark.parametrize("k,cout,act", [(3, 37, "relu"), (1, 70, "gelu"), (3, 136, None), (1, 129, "relu")])
 def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
     """Halo-tiled split-precision conv (cfg 0/1 weights via LDS, 2-5, 8, 9 in registers, 16+c the

@@ -3,7 +3,7 @@ register-weight tiles and fp64 torch.
 
 The pipelined variant changes only WHEN a chunk is split and stored (inside the previous chunk's
 MFMA stream, into the other LDS buffer): the products, their order and the block exponent are the
-plain tile's, so its output must be bit-identical -- checked for every 2D register-weight tile (2..9),
+plain tile's, so its output must be bit-identical -- checked for every 2D register-weight tile (2..9, 11),
 1x1 and 3x3, 1-3 input segments (one a channel slice), ragged rows / columns / couts / channel
 chunks, split-K 1-3, the output-slice / gamma / residual epilogue, and an all-zero first chunk.
 """
@@ -32,7 +32,7 @@ def ops_mod():
     return ops
 
 
-@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6, 7, 8, 9, 11])
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("nsplit", [1, 2, 3])
 def test_pipe_bit_identical(ops_mod, cfg, k, nsplit):
@@ -60,7 +60,7 @@ def test_pipe_bit_identical(ops_mod, cfg, k, nsplit):
     assert not ops_mod.range_overflowed(reset=True)
 
 
-@pytest.mark.parametrize("cfg", [3, 9])
+@pytest.mark.parametrize("cfg", [3, 9, 11])
 def test_pipe_zero_first_chunk(ops_mod, cfg):
     """Chunks 0 and 1 all zero: the exponent comes from chunk 2 (one extra block max + barrier)."""
     B, H, W = 1, 12, 40
@@ -73,3 +73,21 @@ def test_pipe_zero_first_chunk(ops_mod, cfg):
     assert torch.equal(out, plain)
     ref = F.conv2d(x.double(), w.double(), padding=1)
     assert float((out.double().cpu() - ref).abs().max() / ref.abs().max()) < 3e-6
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_tile11_safe_mode(ops_mod, k):
+    """Safe range mode sends the 2D-only 5-row tile (cfg 11 / 43) to the volume instantiation of the
+    4-row 256-cout tile: same conv within the split-precision tolerance."""
+    B, H, W = 1, 15, 40
+    x = torch.randn(B, 96, H, W, generator=torch.Generator().manual_seed(5))
+    w = torch.randn(260, 96, k, k, generator=torch.Generator().manual_seed(6)) * 0.1
+    pk = ops_mod.PackedConv(g(w), mode="halo")
+    ref = F.conv2d(x.double(), w.double(), padding=k // 2)
+    ops_mod.set_range_safe(True)
+    try:
+        outs = [ops_mod.conv2d([x.to(DEV)], pk, cfg=c, nsplit=1) for c in (11, 43)]
+    finally:
+        ops_mod.set_range_safe(False)
+    for out in outs:
+        assert float((out.double().cpu() - ref).abs().max() / ref.abs().max()) < 3e-6

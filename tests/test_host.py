@@ -144,7 +144,9 @@ def test_conv_tuning_db_wellformed():
         # pointwise tiles 24..26 (2D 1x1 layers only), the depth-blocked (17, 1, 1) tile 30, or the
         # pipelined-staging register tiles 32 + (2..9) (conv_halo_x3.hip: volumes fall back to the
         # plain tile)
+        # (11 / 43: the 2D-only 256 x 5-row tile and its pipelined variant)
         assert (0 <= e["cfg"] <= 9 or e["cfg"] in (19, 20, 21, 23)
                 or (24 <= e["cfg"] <= 26 and ks == 1 and kd == 1 and D == 1)
                 or (e["cfg"] == 30 and kd == 17 and ks == 1)
-                or 34 <= e["cfg"] <= 41) and 1 <= e["nsplit"] <= 8, (key, e)
+                or 34 <= e["cfg"] <= 41 or (e["cfg"] in (11, 43) and kd == 1 and D == 1)) \
+            and 1 <= e["nsplit"] <= 8, (key, e)

@@ -41,6 +41,9 @@ ap.add_argument("--write", action="store_true", help="merge the result into tuni
 ap.add_argument("--out", default="", help="also write the merged table here (e.g. under gpurun_out/)")
 ap.add_argument("--nosplit", action="store_true", help="also try each shape's current tile without split-K")
 ap.add_argument("--alts-only", action="store_true", help="skip the isolated candidate search (with --nosplit)")
+ap.add_argument("--match", default="", help="regex: only shapes whose key matches")
+ap.add_argument("--try", dest="try_", nargs="*", default=[],
+                help="cfg:nsplit pairs tried in situ on every searched shape they are legal for (e.g. 43:1 43:2)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 t_start = time.time()
@@ -135,10 +138,11 @@ def candidates(key):
         nck = kd * ((cin + 31) // 32)
         cfgs = ([2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
+                + ([11] if cout > 128 and x.dim() == 4 else [])
                 + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
                 + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
         if x.dim() == 4:                            # pipelined-staging variants of the register tiles
-            cfgs += [32 + c for c in cfgs if 2 <= c <= 9]
+            cfgs += [32 + c for c in cfgs if 2 <= c <= 9 or c == 11]
         if x.dim() == 5 and ks == 1 and kd == 17:   # depth-blocked (17, 1, 1) tile
             cfgs.append(30)
         res = []
@@ -160,8 +164,18 @@ def table_us(key):
     return e.get("us", 0.0) if e else 0.0
 
 
-order = sorted((k for k in counts if "s2" not in k),     # stride-2 tiles keep their s2_bench entries
+order = sorted((k for k in counts if "s2" not in k and re.search(a.match, k)),   # stride-2: s2_bench entries
                key=lambda k: -counts[k] * max(table_us(k), 1.0))[:a.top]
+
+
+def legal(key, c, s):
+    ks, kd, cin, cout, B, D, Hh, Ww = (int(v) for v in re.findall(r"\d+", key))
+    two_d = kd == 1 and D == 1
+    if c in (11, 43) or c >= 32:
+        return two_d and s <= kd * ((cin + 31) // 32)
+    if c == 30:
+        return not two_d and ks == 1 and kd == 17 and s == 1
+    return True
 print(f"[insitu] {len(counts)} conv shapes, searching {len(order)}", file=sys.stderr, flush=True)
 base = min(evaluate(), evaluate())
 start = base
@@ -172,6 +186,10 @@ for n, key in enumerate(order):
     alts, best_alone = candidates(key)
     if a.nosplit and cur is not None and (cur["cfg"], 1) not in alts and cur["cfg"] != 30:
         alts = [(cur["cfg"], 1)] + alts          # no split-K: other streams fill the tail in situ
+    for pair in a.try_:
+        c, s = (int(v) for v in pair.split(":"))
+        if (c, s) not in alts and legal(key, c, s):
+            alts.append((c, s))
     print(f"[insitu] {n + 1}/{len(order)} {key} x{counts[key]}: alternatives {alts}, step {base:.3f} ms "
           f"({(time.time() - t_start) / 60:.1f} min)", file=sys.stderr, flush=True)
     for (c, s) in alts:

@@ -128,10 +128,11 @@ with torch.no_grad():
         nck = kd * ((cin + 31) // 32)
         cfgs = ([2, 3, 4, 5] + ([0, 1] if x.dim() == 4 else []) + ([6, 7] if cout <= 64 else [])
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
+                + ([11] if cout > 128 and x.dim() == 4 else [])
                 + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
                 + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
         if x.dim() == 4:                            # pipelined-staging variants of the register tiles
-            cfgs += [32 + c for c in cfgs if 2 <= c <= 9]
+            cfgs += [32 + c for c in cfgs if 2 <= c <= 9 or c == 11]
         if x.dim() == 5 and ks == 1 and kd == 17:   # depth-blocked (17, 1, 1) tile (no split-K)
             cfgs.append(30)
         splits = [s for s in (1, 2, 3, 4, 6, 8) if s <= max(1, nck) and s <= a.max_split]
