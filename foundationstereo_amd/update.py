@@ -76,6 +76,9 @@ def _packed(*mods, cin_order=None):
 
 
 _SIDE = {}
+# A/B knob: the motion stream (lookup + motion encoder, the loop's critical path) at high priority,
+# so its blocks are dispatched ahead of the concurrently queued gru16 / gru08 conv blocks
+MOTION_PRIORITY = int(os.environ.get("FSMI_MOT_PRIO", "0"))
 
 
 def _side_stream(device, idx=0):
@@ -83,7 +86,8 @@ def _side_stream(device, idx=0):
     gru16 / gru08 pipeline of ``run_pipelined``)."""
     s = _SIDE.get((device, idx))
     if s is None:
-        s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device)
+        prio = -MOTION_PRIORITY if idx == 0 else 0       # lower number = higher priority
+        s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device, priority=prio)
     return s
 
 

@@ -129,6 +129,29 @@ def test_build_stem_tiles(ops_mod, vit, W, D, tile, monkeypatch):
     close(out, ref, atol=2e-5)
 
 
+@pytest.mark.parametrize("vit,B,H", [("vits", 1, 135), ("vitl", 2, 150)])
+def test_build_stem_persistent(ops_mod, vit, B, H):
+    """More tiles than one round of the 256 CUs: the persistent build (each block walks several tiles,
+    prefetching the next tile's operands during the current one's stores; 2 and 3 tiles per block,
+    one and two group phases) == the oracle's Conv3d_1x1(cat(gwc, concat(proj(fl), proj(fr))))."""
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    W, D = 160, 48
+    args = synth.make_args(max_disp=4 * D, corr_levels=2, vit_size=vit)
+    m = FoundationStereo(args)
+    synth.init_module_(m, seed=7)
+    m = m.to(DEV).eval()
+    C = m.feature.d_out[0]
+    fl, fr = synth.normal(41, (B, C, H, W)), synth.normal(42, (B, C, H, W))
+    with torch.no_grad():
+        out = m.build_stem_volume(g(fl), g(fr))
+        P = {k: v.cpu() for k, v in m.state_dict().items()}
+        comb = torch.cat([oracle.build_gwc_volume(t(fl), t(fr), D, 8),
+                          oracle.build_concat_volume(oracle.stereo_oracle._conv(P, "proj_cmb", t(fl)),
+                                                     oracle.stereo_oracle._conv(P, "proj_cmb", t(fr)), D)], 1)
+        ref = oracle.stereo_oracle._conv(P, "corr_stem.0", comb)
+    close(out, ref, atol=2e-5)
+
+
 @pytest.mark.parametrize("KS,shape", [(7, (1, 14, 12, 16, 40)), (7, (2, 5, 5, 9, 33)), (3, (1, 14, 8, 8, 64))])
 def test_conv3d_direct_vs_torch(ops_mod, KS, shape):
     """Classifier head Conv3d(Cin, 1, KS, padding=KS//2) vs the fp32 torch CPU conv (ragged tiles included)."""

@@ -10,6 +10,7 @@
 #   pmc         FETCH_SIZE / WRITE_SIZE passes (one counter per run) + tools/pmc_summary.py, cfg2
 #   sq          SQ_ counters (MFMA busy, instruction mix) over the conv kernels, cfg2
 #   smoke       __graft_entry__.smoke()
+#   ab          A/B of environment settings on the bench (AB_ENVS="K=V;K=V2", AB_REPS rounds)
 #   py:<file>   python3 <file> (a tool script), output to <file base>.out
 # Every GPU step runs under its own timeout and the script stops at the first failing step.
 set -o pipefail
@@ -62,6 +63,18 @@ for step in "$@"; do
       done
       python3 tools/conv_pmc_summary.py $OUT --top 16 --out $OUT/sq_cfg2.json > $OUT/sq_table.txt
       cat $OUT/sq_table.txt ;;
+    ab)
+      # A/B of environment settings on the cfg2 bench: AB_ENVS="K=V K2=V2;K=V3" (';' separates the arms),
+      # AB_REPS rounds of every arm in turn
+      IFS=';' read -ra ARMS <<< "${AB_ENVS}"
+      for r in $(seq 1 ${AB_REPS:-2}); do
+        for i in "${!ARMS[@]}"; do
+          arm="${ARMS[$i]}"
+          timeout -k 10 300 env $arm python3 bench.py --config ${AB_CONFIG:-cfg2} --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline $BENCH_ARGS \
+            > $OUT/ab_${i}_$r.json 2> $OUT/ab_${i}_$r.err || fail "ab arm $i" $? $OUT/ab_${i}_$r.err
+          echo "arm $i [$arm] round $r: $(python3 tools/bench_brief.py $OUT/ab_${i}_$r.json)"
+        done
+      done ;;
     py:*)
       f=${step#py:}; b=$(basename $f .py)
       timeout -k 10 ${PY_TIMEOUT:-400} python3 -u $f ${PY_ARGS:-} > $OUT/$b.out 2> $OUT/$b.err || fail "$f" $? $OUT/$b.err
