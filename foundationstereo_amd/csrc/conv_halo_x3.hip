@@ -160,7 +160,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     // take the 128 x 2 x 32 register-weight tile
     d3 = true;
     if (cfg == 11 || cfg == 43) cfg = 9;           // the 5-row tile is 2D only
-    else if (cfg >= 24 && cfg <= 26) cfg = 4;      // (pipelined 32 + c: the plain tile c, below)
+    else if (cfg >= 24 && cfg <= 29) cfg = 4;      // (pipelined 32 + c: the plain tile c, below)
   }
   if (cfg == 30) {                                 // depth-blocked (17, 1, 1) tile (conv_depth.hip)
     FSMI_CHECK_ARG(d3 && KS == 1 && KD == 17 && a.str == 1 && !a.up, "%s: tile 30 takes (17, 1, 1) stride-1 "
@@ -184,7 +184,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   }
   const bool pw = cfg >= 24;
   if (pw) {                                        // pointwise LDS-DMA tiles (conv_pw.hip)
-    FSMI_CHECK_ARG(cfg <= 26 && KS == 1 && !d3 && HW % 4 == 0, "%s: pointwise tile %d needs a 2D 1x1 conv with "
+    FSMI_CHECK_ARG(cfg <= 29 && KS == 1 && !d3 && HW % 4 == 0, "%s: pointwise tile %d needs a 2D 1x1 conv with "
                    "H*W %% 4 == 0", what, cfg);
     for (int i = 0; i < nseg; ++i)
       FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(seg_ptr[i]) % 16 == 0, "%s: pointwise tile needs 16-B aligned "
@@ -197,7 +197,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     FSMI_CHECK_ARG(halo::kg2_tile(cfg), "%s: tile %d has no K-group variant (16 + 3/4/5/7)", what, cfg);
   }
   FSMI_CHECK_ARG((cfg >= 0 && cfg <= 9) || pw || (a.str == 2 && cfg == 10) || (cfg == 11 && !d3 && KS != 2),
-                 "%s: cfg %d (0..9, 11 on 2D maps, 16 + 3/4/5/7, 24..26)", what, cfg);
+                 "%s: cfg %d (0..9, 11 on 2D maps, 16 + 3/4/5/7, 24..29)", what, cfg);
   FSMI_CHECK_ARG(a.str == 1 || (kg == 1 && (cfg == 4 || cfg == 5 || cfg == 7 || cfg == 10)),
                  "%s: stride-2 tile %d (4, 5, 7, 10)", what, cfg);
   if (pw) halo::pw_tile(cfg, a);

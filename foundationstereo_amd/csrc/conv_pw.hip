@@ -52,14 +52,23 @@ __device__ __forceinline__ void dma16(const float* src, float* dst) {
 // every LDS-DMA chunk in flight, and serialise the ring; the waits are explicit instead
 __device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int BM, int PX, int WM, int NS>
+// COOP (cfg 27-29): the block splits each chunk ONCE -- every thread converts 8 channels of one
+// pixel of the fp32 ring slot into fp16 hi / lo and stores them to a double-buffered [pixel][channel]
+// image (the halo tiles' 80-B rows: conflict-free ds_read_b128 B fragments) -- instead of every wave
+// splitting the B fragments it reads (WM waves re-split the same pixels: 2 x at cfg 24, 4 x for a
+// 256-cout tile).  Two barriers per chunk; two or three blocks per CU overlap one block's split with
+// another's MFMAs.
+template <int BM, int PX, int WM, int NS, bool COOP = false>
 __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
   constexpr int WN = 4 / WM, TM = BM / WM / 32, TN = PX / WN / 32;
   constexpr int CHF = HKC * PX;                    // floats per chunk: 32 channel rows x PX pixels
   constexpr int OPS = CHF / (4 * 256);             // DMA instructions per wave per chunk (16 B a lane)
   static_assert(TM >= 1 && TN >= 1 && OPS >= 1 && CHF % 1024 == 0 && NS >= 3, "pw tile");
+  static_assert(!COOP || PX * (HKC / 8) % 256 == 0, "coop split: whole 8-channel tasks per thread");
   __shared__ __attribute__((aligned(16))) float ring[NS][CHF];
   __shared__ __attribute__((aligned(16))) float red[4];
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[COOP ? 2 : 1][COOP ? PX : 1][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[COOP ? 2 : 1][COOP ? PX : 1][HROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM, hsel = lane >> 5, rl = lane & 31;
   const long long HW = a.cstride;
@@ -178,6 +187,30 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
       sx = __builtin_amdgcn_readfirstlane(chunk_exp<kRangeHeadroom>(red4_max(red)));
       scale = exp2i(sx == kNoExp ? 0 : sx);
     }
+    if constexpr (COOP) {
+      // the block's one split of chunk q: task = (8-channel group g, pixel), ring rows g*8 .. g*8+7
+#pragma unroll
+      for (int u = 0; u < PX * (HKC / 8) / 256; ++u) {
+        const int task = u * 256 + tid, px = task % PX, gq = task / PX;
+        const int nvalid = a.Cin - c * HKC - 8 * gq;
+        const bool pok = px0 + px < HW;
+        f32x8 x;
+        float mx = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float v = xs[(8 * gq + t) * PX + px];
+          x[t] = (t < nvalid && pok) ? v * scale : 0.f;
+          mx = fmaxf(mx, fabsf(x[t]));
+        }
+        ovf |= mx >= 65504.f;
+        const half8 hi = __builtin_convertvector(x, half8);
+        *reinterpret_cast<half8*>(&Xh[P][px][8 * gq]) = hi;
+        if constexpr (FSMI_NPROD == 3)
+          *reinterpret_cast<half8*>(&Xl[P][px][8 * gq]) = __builtin_convertvector(x - __builtin_convertvector(hi, f32x8), half8);
+      }
+      wait_lgkm0();
+      bar();                                       // the split image of chunk q is complete
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       half8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -185,6 +218,16 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
       for (int i = 0; i < TM; ++i) {
         ah[i] = wf[P][i][k][0];
         al[i] = wf[P][i][k][1];
+      }
+      if constexpr (COOP) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int pl = (wn * TN + j) * 32 + rl;
+          bh[j] = *reinterpret_cast<const half8*>(&Xh[P][pl][16 * k + 8 * hsel]);
+          if constexpr (FSMI_NPROD == 3) bl[j] = *reinterpret_cast<const half8*>(&Xl[P][pl][16 * k + 8 * hsel]);
+        }
+        mma3<TM, TN>(acc, ah, al, bh, bl);
+        continue;
       }
       const int ci0 = 16 * k + 8 * hsel;
       const int nvalid = a.Cin - c * HKC - ci0;    // channels of this lane's 8 that exist
@@ -267,7 +310,9 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
 namespace halo {
 
 // cfg 24: 128 couts x 128 px (2 x 2 fragments per wave), 3-deep ring; 25: 128 x 64 (2 x 1), 4 deep;
-// 26: 64 x 128 (2 x 1, waves along the pixels), 3 deep.  Deeper rings (6 / 8 chunks, 64-96 KB of
+// 26: 64 x 128 (2 x 1, waves along the pixels), 3 deep.  The block-split (COOP) tiles: 27: 256 x 64
+// (2 x 2 per wave, waves along the couts), 4 deep; 28: 128 x 64 (2 x 1), 4 deep; 29: 128 x 128
+// (2 x 2), 3 deep.  Deeper rings (6 / 8 chunks, 64-96 KB of
 // LDS) measured 5-40 % slower on every cfg2 1x1 shape (tools/pw_bench.py), so the chunk round
 // trip is not what bounds these layers.  Tile geometry (a.nct = pixel tiles per image, a.npix, a.nco) is set by
 // the caller (pw_tile).
@@ -277,13 +322,16 @@ int launch_pw(int cfg, const HaloArgs& a, hipStream_t s) {
     case 24: hipLaunchKernelGGL((conv_pw_kernel<128, 128, 2, 3>), dim3(grid), dim3(256), 0, s, a); break;
     case 25: hipLaunchKernelGGL((conv_pw_kernel<128, 64, 2, 4>), dim3(grid), dim3(256), 0, s, a); break;
     case 26: hipLaunchKernelGGL((conv_pw_kernel<64, 128, 1, 3>), dim3(grid), dim3(256), 0, s, a); break;
-    default: set_error("fsmi_conv_halo: pointwise tile %d (24..26)", cfg); return FSMI_ERR_ARG;
+    case 27: hipLaunchKernelGGL((conv_pw_kernel<256, 64, 4, 4, true>), dim3(grid), dim3(256), 0, s, a); break;
+    case 28: hipLaunchKernelGGL((conv_pw_kernel<128, 64, 2, 4, true>), dim3(grid), dim3(256), 0, s, a); break;
+    case 29: hipLaunchKernelGGL((conv_pw_kernel<128, 128, 2, 3, true>), dim3(grid), dim3(256), 0, s, a); break;
+    default: set_error("fsmi_conv_halo: pointwise tile %d (24..29)", cfg); return FSMI_ERR_ARG;
   }
   return finish_launch("fsmi_conv_halo");
 }
 
 void pw_tile(int cfg, HaloArgs& a) {
-  const int BM = cfg == 26 ? 64 : 128, PX = cfg == 25 ? 64 : 128;
+  const int BM = cfg == 26 ? 64 : cfg == 27 ? 256 : 128, PX = (cfg == 25 || cfg == 27 || cfg == 28) ? 64 : 128;
   const long long HW = a.cstride;
   a.nrt = 1;
   a.nct = static_cast<int>((HW + PX - 1) / PX);

@@ -194,10 +194,10 @@ def test_conv2d_halo_vs_torch(ops_mod, cfg, k, cout, act, nsplit, HW):
 
 @pytest.mark.parametrize("HW", [(12, 40), (16, 64)])
 @pytest.mark.parametrize("nsplit", [1, 2, 3])
-@pytest.mark.parametrize("cfg", [24, 25, 26])
+@pytest.mark.parametrize("cfg", [24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("cout,act,wide", [(70, "gelu", False), (129, "relu", True), (256, None, True)])
 def test_conv2d_pw_vs_torch(ops_mod, cfg, cout, act, wide, nsplit, HW):
-    """Pointwise LDS-DMA tiles (conv_pw.hip, cfg 24-26): 2 or 3 segments (16 channels, optionally
+    """Pointwise LDS-DMA tiles (conv_pw.hip, cfg 24-26; 27-29 split once per block): 2 or 3 segments (16 channels, optionally
     160 more, a 29-channel slice: 2 or 7 chunks through the 3/4-deep ring, ragged last chunk), pixel
     tiles past the plane end (480 px), ragged couts, output slice, every epilogue term, split-K;
     vs fp64 torch, same tolerance as the halo tiles."""
@@ -347,7 +347,7 @@ def test_hourglass_gated_vs_unfused(ops_mod):
 
 
 @pytest.mark.parametrize("scale", [3e5, 1e3, 1e-4, 1e-7])
-@pytest.mark.parametrize("cfg", [24, 25, 26])
+@pytest.mark.parametrize("cfg", [24, 25, 26, 27, 28, 29])
 def test_conv2d_pw_range(ops_mod, scale, cfg):
     """Pointwise tiles keep ~22 bits across input scales (block exponent from the first chunk)."""
     import torch.nn.functional as F

@@ -49,7 +49,7 @@ def _rel_err(out, ref):
     return float((out.double().cpu() - ref).abs().max() / ref.abs().max())
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 3, 4, 9, 19, 24, 25, 26])
+@pytest.mark.parametrize("cfg", [-1, 1, 3, 4, 9, 19, 24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("k", [1, 3])
 def test_safe_mode_conv2d(lib, cfg, k):
     """[small chunk, chunk 1e7 x larger]: mode 2 flags it; safe mode computes it to ~22 bits."""

@@ -146,7 +146,7 @@ def test_conv_tuning_db_wellformed():
         # plain tile)
         # (11 / 43: the 2D-only 256 x 5-row tile and its pipelined variant)
         assert (0 <= e["cfg"] <= 9 or e["cfg"] in (19, 20, 21, 23)
-                or (24 <= e["cfg"] <= 26 and ks == 1 and kd == 1 and D == 1)
+                or (24 <= e["cfg"] <= 29 and ks == 1 and kd == 1 and D == 1)
                 or (e["cfg"] == 30 and kd == 17 and ks == 1)
                 or 34 <= e["cfg"] <= 41 or (e["cfg"] in (11, 43) and kd == 1 and D == 1)) \
             and 1 <= e["nsplit"] <= 8, (key, e)

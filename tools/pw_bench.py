@@ -15,7 +15,7 @@ from foundationstereo_amd import ops  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
-ap.add_argument("--cfgs", type=int, nargs="*", default=[24, 25, 26])
+ap.add_argument("--cfgs", type=int, nargs="*", default=[24, 25, 26, 27, 28, 29])
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 SHAPES = [(512, 128, 120, 160), (1044, 256, 120, 160), (128, 512, 120, 160), (512, 256, 120, 160),

@@ -91,7 +91,7 @@ if a.set in ("loop", "all"):
             for c in (3, 4, 9):
                 cands += [(c, tns), (c + 32, tns)]
         if k == 1:
-            cands += [(c, ns) for c in (24, 25, 26) for ns in (1, 2, 3) if (c, ns) != (tcfg, tns)]
+            cands += [(c, ns) for c in (24, 25, 26, 27, 28, 29) for ns in (1, 2, 3) if (c, ns) != (tcfg, tns)]
         fl = 2.0 * cin * cout * k * k * H * W
         for cfg, ns in cands:
             fn = lambda: ops.conv2d([x], pk, bias=b, act="relu", cfg=cfg, nsplit=ns)  # noqa: E731

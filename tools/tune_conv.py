@@ -130,7 +130,7 @@ with torch.no_grad():
                 + ([8] if cout > 64 else []) + ([9] if cout > 128 else [])
                 + ([11] if cout > 128 and x.dim() == 4 else [])
                 + [16 + c for c in (3, 4, 5) + ((7,) if cout <= 64 else ()) if nck >= 2]
-                + ([24, 25, 26] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
+                + ([24, 25, 26, 27, 28, 29] if ks == 1 and x.dim() == 4 and (Hh * Ww) % 4 == 0 else []))
         if x.dim() == 4:                            # pipelined-staging variants of the register tiles
             cfgs += [32 + c for c in cfgs if 2 <= c <= 9 or c == 11]
         if x.dim() == 5 and ks == 1 and kd == 17:   # depth-blocked (17, 1, 1) tile (no split-K)
