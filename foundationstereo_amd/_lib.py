@@ -58,6 +58,7 @@ SIGNATURES = {
     "fsmi_set_range_safe": [_I],
     "fsmi_range_poison": [_P, ctypes.c_longlong, _P],
     "fsmi_get_range_safe": [ctypes.POINTER(_I)],
+    "fsmi_conv_launch_counts": [ctypes.POINTER(ctypes.c_longlong), _I, _I],
     "fsmi_timer_enable": [_I],
     "fsmi_timer_reset": [],
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],

@@ -1,5 +1,7 @@
 // Halo-tiled split-precision convolution: host side (tile / split-K policy, C ABI entry points)
 // and the split-K reduce pass.  Device code and its description: conv_halo.h.
+#include <atomic>
+
 #include "conv_halo.h"
 
 namespace fsmi {
@@ -94,6 +96,9 @@ using namespace fsmi;
 namespace {
 
 unsigned long long* g_conv_ts = nullptr;
+// launches per tile config as launched (0..9 and 11 register / LDS tiles, 10 stride-2, 16 + c K groups,
+// 24..29 pointwise, 30 depth-blocked, 32 + c pipelined): fsmi_conv_launch_counts
+std::atomic<long long> g_cfg_launches[64];
 
 // Shared host side of both entry points: validates, fills HaloArgs (gate fields preset by the
 // caller), picks tiles and split-K, launches.
@@ -170,6 +175,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     a.ws = nullptr;
     a.ts = nullptr;
     a.ovf = range_flag_device();
+    g_cfg_launches[30].fetch_add(1, std::memory_order_relaxed);
     const int rc = halo::launch_depth(a, s);
     if (rc != FSMI_OK) return rc;
     return finish_launch(what);
@@ -249,6 +255,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     return e ? std::atoi(e) : 0;
   }();
   a.dbg = conv_dbg;
+  g_cfg_launches[(a.pipe ? 32 : 0) + (kg == 2 ? 16 : 0) + cfg].fetch_add(1, std::memory_order_relaxed);
   const int rc = a.str == 2 ? halo::launch_s2(KS, cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
@@ -261,6 +268,14 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
 // Debug: while buf is non-NULL every halo conv launch records, per block, thread 0's wall clock
 // (100 MHz) at start [0], at each chunk's staging barrier [1..36], before / after the epilogue
 // [37] / [38] and (chunks << 32 | block) [39] into buf[block * 40 ..] (tools/conv_phases.py).
+extern "C" int fsmi_conv_launch_counts(long long* counts, int n, int reset) {
+  FSMI_CHECK_ARG(counts && n > 0 && n <= 64, "fsmi_conv_launch_counts: 1..64 counters");
+  for (int i = 0; i < n; ++i) counts[i] = g_cfg_launches[i].load(std::memory_order_relaxed);
+  if (reset)
+    for (auto& c : g_cfg_launches) c.store(0, std::memory_order_relaxed);
+  return FSMI_OK;
+}
+
 extern "C" int fsmi_debug_conv_timestamps(unsigned long long* buf) {
   g_conv_ts = buf;
   return FSMI_OK;

@@ -778,6 +778,15 @@ def guarded(run):
     return out
 
 
+def conv_launch_counts(reset: bool = False) -> List[int]:
+    """Halo / pointwise / depth conv launches per tile config since the last reset (64 counters,
+    fsmi_conv_launch_counts): which tile the tuning table or the policy actually ran."""
+    import ctypes
+    buf = (ctypes.c_longlong * 64)()
+    _lib.check(_lib.load().fsmi_conv_launch_counts(buf, 64, 1 if reset else 0), "conv_launch_counts")
+    return list(buf)
+
+
 # ---------------------------------------------------------------- timing
 
 # algorithmic fp32 conv FLOPs (2*Cin*Cout*k*k*B*H*W) of the conv2d calls made since the last

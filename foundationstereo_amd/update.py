@@ -76,9 +76,6 @@ def _packed(*mods, cin_order=None):
 
 
 _SIDE = {}
-# A/B knob: the motion stream (lookup + motion encoder, the loop's critical path) at high priority,
-# so its blocks are dispatched ahead of the concurrently queued gru16 / gru08 conv blocks
-MOTION_PRIORITY = int(os.environ.get("FSMI_MOT_PRIO", "0"))
 
 
 def _side_stream(device, idx=0):
@@ -86,8 +83,9 @@ def _side_stream(device, idx=0):
     gru16 / gru08 pipeline of ``run_pipelined``)."""
     s = _SIDE.get((device, idx))
     if s is None:
-        prio = -MOTION_PRIORITY if idx == 0 else 0       # lower number = higher priority
-        s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device, priority=prio)
+        # all at default priority: the motion stream at high priority (its lookup dispatched ahead
+        # of the pipeline stream's conv blocks) measured 14.7 vs 19.0 pairs/s (round 4)
+        s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device)
     return s
 
 

@@ -171,6 +171,13 @@ int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float*
  * epilogue.  ws may be NULL when nsplit is 0/1 (or auto: then no split).
  * (A last-arriving-block fixup inside the conv kernel was measured 4x slower:
  * the agent-scope fences it needs flush and invalidate the per-XCD L2.) */
+/* Launches of the halo / pointwise / depth conv tiles since the last reset, per tile config as
+ * launched: counts[c] for c < n (n <= 64): 0..9 and 11 register / LDS tiles, 10 stride-2 tiles,
+ * 16 + c K-group tiles, 24..29 pointwise tiles, 30 the depth-blocked (17,1,1) tile, 32 + c the
+ * pipelined variant of tile c.  reset != 0 zeroes them after the read.  (Which tile the tuning table
+ * or the policy picked for a layer, checked by tests.) */
+int fsmi_conv_launch_counts(long long* counts, int n, int reset);
+
 /* Debug: while buf != NULL, every halo-conv launch stores per-block wall-clock
  * stamps (100 MHz) into buf[block*40 + 0..39]: start, each chunk's staging
  * barrier, before/after the epilogue, (chunks << 32 | block).  NULL disables. */

@@ -95,3 +95,23 @@ def test_depth_conv_plane_range(ops_mod):
     # per output depth, relative to that depth's own magnitude (the window spans ~4 decades)
     rel = ((out.double().cpu() - ref).abs().amax((0, 1, 3, 4)) / ref.abs().amax((0, 1, 3, 4)))
     assert float(rel.max()) < 1e-4, rel
+
+
+@pytest.mark.parametrize("cin,D,H,W,name", [(28, 48, 120, 160, "cfg2 conv_out / agg_0"),
+                                            (56, 24, 60, 80, "cfg2 hourglass 1/8 (17,1,1)")])
+def test_product_selects_depth_tile(ops_mod, cin, D, H, W, name):
+    """What the product runs for cfg2's (17, 1, 1) convs: the tuning table's in-situ entry picks
+    the depth tile (cfg 30) for these shapes, and the launch counters show conv_depth_kernel ran
+    (not the generic volume tile) -- the same call path as Conv3dNormActReduced.conv2 (ops.conv3d,
+    cfg / nsplit on auto).  Output agrees with the generic tile 7."""
+    cfg, nsplit = ops_mod._tuned(1, 17, cin, cin, 1, D, H, W, -1, -1)
+    assert (cfg, nsplit) == (30, 1), (name, cfg, nsplit)
+    x, w, bias = _case(cin, cin, D, H, W, 1, cin + D)
+    pk = ops_mod.PackedConv(g(w), mode="halo")
+    ops_mod.conv_launch_counts(reset=True)
+    out = ops_mod.conv3d(g(x), pk, bias=g(bias), act="relu")
+    torch.cuda.synchronize()
+    counts = ops_mod.conv_launch_counts(reset=True)
+    assert counts[30] == 1 and sum(counts) == 1, [(i, c) for i, c in enumerate(counts) if c]
+    generic = ops_mod.conv3d(g(x), pk, bias=g(bias), act="relu", cfg=7, nsplit=1)
+    close(out, generic, atol=2e-5, rtol=1e-5)

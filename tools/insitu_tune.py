@@ -171,10 +171,17 @@ order = sorted((k for k in counts if "s2" not in k and re.search(a.match, k)),  
 def legal(key, c, s):
     ks, kd, cin, cout, B, D, Hh, Ww = (int(v) for v in re.findall(r"\d+", key))
     two_d = kd == 1 and D == 1
+    nck = kd * ((cin + 31) // 32)
+    if s > nck:
+        return False
     if c in (11, 43) or c >= 32:
-        return two_d and s <= kd * ((cin + 31) // 32)
+        return two_d
+    if 24 <= c <= 29:
+        return two_d and ks == 1 and (Hh * Ww) % 4 == 0
     if c == 30:
         return not two_d and ks == 1 and kd == 17 and s == 1
+    if 16 <= c < 24:
+        return 2 * s <= nck
     return True
 print(f"[insitu] {len(counts)} conv shapes, searching {len(order)}", file=sys.stderr, flush=True)
 base = min(evaluate(), evaluate())
