@@ -418,6 +418,31 @@ __device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], i
 
 // ---------------------------------------------------------------- shared pieces
 
+// The input segments (zero-copy cat) of batch b as uniform base pointers: channel ci (of the
+// concatenated input) at element offset `off` of its plane is p[q] + ci * HW + off, q the segment
+// holding ci -- p[q] is segment q's pointer for batch b moved back by its first channel's HW
+// multiple.  Computed once per staging call from kernel arguments (scalar registers); per lane
+// only the segment select and one multiply-add remain (the per-lane select of pointer, batch
+// stride and first channel plus two 64-bit products was ~60 VALU per 8-channel task).
+struct SegBases {
+  uintptr_t p[kHMaxSeg];
+  __device__ __forceinline__ void init(const HaloArgs& a, int b, long long HW) {
+    int start = 0;
+#pragma unroll
+    for (int q = 0; q < kHMaxSeg; ++q) {
+      p[q] = reinterpret_cast<uintptr_t>(a.seg_ptr[q]) +
+             static_cast<uintptr_t>(b * a.seg_bstride[q] - static_cast<long long>(start) * HW) * sizeof(float);
+      start = a.seg_end[q];
+    }
+  }
+  __device__ __forceinline__ const float* chan(const HaloArgs& a, int ci, long long HW) const {
+    uintptr_t sp = p[0];
+#pragma unroll
+    for (int q = 1; q < kHMaxSeg; ++q) sp = (q < a.nseg && ci >= a.seg_end[q - 1]) ? p[q] : sp;
+    return reinterpret_cast<const float*>(sp) + static_cast<long long>(ci) * HW;
+  }
+};
+
 // Input-halo staging for a TR x 32 pixel tile: task = (halo pixel, 8-channel
 // group); per task a packed descriptor (clamped pixel offset << 3 | in-image << 2
 // | group) computed once per block; a chunk is loaded into registers one chunk
@@ -452,24 +477,16 @@ struct HaloStage {
     const bool plane_ok = d >= 0 && d < ID;
     const long long poff = static_cast<long long>(min(max(d, 0), ID - 1)) *
                            (STR == 1 ? a.H * a.W : a.iH * a.iW);
+    SegBases seg;
+    seg.init(a, b, HW);
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u) {
       const int g = desc[u] & 3, pix = desc[u] >> 3;
       const int ci0 = cc * HKC + g * 8;
       const int cic = min(ci0, a.Cin - 1);
-      // segment of this 8-channel group (segments hold multiples of 8 channels): a select
-      // chain over constant indices, so the kernarg arrays are never indexed per lane
-      const float* sp = a.seg_ptr[0];
-      long long sb = a.seg_bstride[0];
-      int base = 0;
-#pragma unroll
-      for (int q = 1; q < kHMaxSeg; ++q) {
-        const bool in_q = q < a.nseg && cic >= a.seg_end[q - 1];
-        sp = in_q ? a.seg_ptr[q] : sp;
-        sb = in_q ? a.seg_bstride[q] : sb;
-        base = in_q ? a.seg_end[q - 1] : base;
-      }
-      const float* src = sp + b * sb + static_cast<long long>(cic - base) * HW + poff + pix;
+      // segment of this 8-channel group (segments hold multiples of 8 channels): a select chain
+      // over constant indices, so the kernarg arrays are never indexed per lane
+      const float* src = seg.chan(a, cic, HW) + poff + pix;
       const bool ok = (desc[u] & 4) && plane_ok;
       f32x8 v;
       if (full) {

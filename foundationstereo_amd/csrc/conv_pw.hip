@@ -94,22 +94,13 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
     drow[o] = e / PX;
     dpix[o] = min(px0 + e % PX, HW - 4);           // a tile tail past the plane re-reads its last quad
   }
+  SegBases seg;
+  seg.init(a, b, HW);
   auto dma = [&](int c, int slot) FSMI_HALO_INL {
 #pragma unroll
     for (int o = 0; o < OPS; ++o) {
       const int ci = min(c * HKC + drow[o], a.Cin - 1);   // channels past Cin: any valid row (zeroed below)
-      const float* sp = a.seg_ptr[0];
-      long long sb = a.seg_bstride[0];
-      int base = 0;
-#pragma unroll
-      for (int q = 1; q < kHMaxSeg; ++q) {
-        const bool in_q = q < a.nseg && ci >= a.seg_end[q - 1];
-        sp = in_q ? a.seg_ptr[q] : sp;
-        sb = in_q ? a.seg_bstride[q] : sb;
-        base = in_q ? a.seg_end[q - 1] : base;
-      }
-      const float* src = sp + b * sb + static_cast<long long>(ci - base) * HW + dpix[o];
-      dma16(src, &ring[slot][(wave * OPS + o) * 256]);
+      dma16(seg.chan(a, ci, HW) + dpix[o], &ring[slot][(wave * OPS + o) * 256]);
     }
   };
 

@@ -91,3 +91,54 @@ def test_sharded_real_model_world2():
         assert eager.shape == (2, 1, H, W)
         np.testing.assert_allclose(eager, single, atol=1e-4, rtol=0)    # batch invariance (fp32 order)
         np.testing.assert_allclose(replay, eager, atol=1e-5, rtol=0)     # graph == eager
+
+
+def _nccl_worker(port, q):
+    import torch.distributed as dist
+    from foundationstereo_amd import dist as fdist, ops, synth
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    rank, _, world = fdist.init_from_env("nccl", force=True)
+    try:
+        assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+        m = _model(seed=1234)
+        fdist.broadcast_module_(m, src=0)
+        m.feature.set_features(*_features(0, 2))
+        left, right = synth.stereo_images(2, H, W)
+        batch = torch.from_numpy(np.stack([left, right], 1)).to("cuda:0")
+        runner = fdist.ShardedStereo(lambda lf, rt: m(lf, rt, iters=ITERS, test_mode=True), rank, world)
+        with torch.no_grad():
+            eager = runner.step(batch, (1, H, W)).cpu()
+            runner.capture(batch)
+            replay = runner.step(batch, (1, H, W)).cpu()
+        q.put((eager.numpy(), replay.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_real_model_rccl_world1():
+    """The "nccl" (RCCL) branch of ShardedStereo on hardware: a process group of one rank, so the
+    step's scatter and all_gather_into_tensor run as RCCL collectives on device tensors (the 8-GPU
+    path bench.py takes under torchrun), eagerly and around a captured replay; same result as the
+    single-process forward."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        eager, replay = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    from foundationstereo_amd import synth
+    m = _model(seed=1234)
+    m.feature.set_features(*_features(0, 2))
+    left, right = synth.stereo_images(2, H, W)
+    with torch.no_grad():
+        single = m(torch.from_numpy(left).cuda(), torch.from_numpy(right).cuda(), iters=ITERS,
+                   test_mode=True).cpu().numpy()
+    assert eager.shape == (2, 1, H, W)
+    np.testing.assert_allclose(eager, single, atol=1e-5, rtol=0)
+    np.testing.assert_allclose(replay, eager, atol=1e-5, rtol=0)

@@ -24,7 +24,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     test)
-      timeout -k 10 1100 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TEST_ARGS:-} \
+      timeout -k 10 1100 python3 -u -m pytest ${TEST_PATHS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread ${TEST_ARGS:-} \
         > $OUT/test.log 2>&1 || fail test $? $OUT/test.log
       tail -3 $OUT/test.log ;;
     smoke)
