@@ -359,8 +359,17 @@ def test_conv2d_pw_range(ops_mod, scale, cfg):
     for nsplit in (1, 2):
         out = ops_mod.conv2d([g(x)], ops_mod.PackedConv(g(w), mode="halo"), cfg=cfg, nsplit=nsplit)
         assert bool(torch.isfinite(out).all())
-        err = float((out.double().cpu() - ref).abs().max() / ref.abs().max())
-        assert err < 3e-6, (nsplit, err)
+        d = (out.double().cpu() - ref).abs() / ref.abs().max()
+        err = float(d.max())
+        if err >= 3e-6:
+            # diagnostics for an intermittent failure: where, how many, and whether the same call
+            # reproduces it right away (same inputs, same stream)
+            idx = int(d.argmax())
+            again = ops_mod.conv2d([g(x)], ops_mod.PackedConv(g(w), mode="halo"), cfg=cfg, nsplit=nsplit)
+            err2 = float(((again.double().cpu() - ref).abs() / ref.abs().max()).max())
+            bad = int((d >= 3e-6).sum())
+            raise AssertionError(f"nsplit {nsplit}: err {err:.3e} at (co {(idx // (H * W)) % cout}, px {idx % (H * W)}), "
+                                 f"{bad} bad elements; immediate re-run err {err2:.3e}")
     assert not ops_mod.range_overflowed(reset=True)
 
 
