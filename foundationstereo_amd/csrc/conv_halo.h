@@ -1320,10 +1320,11 @@ __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
         constexpr int k = decltype(k_c)::value, S = 2 * tap + k;
         if constexpr (S + 1 < 2 * NTAP) read_b(std::integral_constant<int, S + 1>());   // next step's B
         half8 ah[TM], al[TM];
+        constexpr int wb = (tap + PP) & 1;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          ah[i] = wf[(tap + PP) & 1][i][k][0];
-          al[i] = wf[(tap + PP) & 1][i][k][1];
+          ah[i] = wf[wb][i][k][0];
+          al[i] = wf[wb][i][k][1];
         }
         mma3<TM, TN>(acc, ah, al, bh[S & 1], bl[S & 1]);
       });

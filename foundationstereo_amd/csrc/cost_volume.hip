@@ -13,10 +13,6 @@
 
 #include "fsmi_common.h"
 
-// build_dma16 writes m0 (the LDS-DMA base): nothing else in this file's kernels uses it
-#pragma clang diagnostic ignored "-Winline-asm"
-#define FSMI_BUILD_INL __attribute__((always_inline))
-
 namespace fsmi {
 namespace {
 
@@ -289,74 +285,12 @@ __device__ __forceinline__ void build_stage_rows(const float* __restrict__ f, si
   }
 }
 
-// build_stage_rows' LDS-DMA issued as inline asm (VEC 4 only): the persistent build prefetches the
-// next tile with these while the current tile's stores drain.  The compiler neither counts them nor
-// guards later LDS reads with its own vmcnt(0) (it cannot tell the prefetch's LDS region from the
-// regions the store loop reads); the one wait on them is explicit (build_wait_prefetch).
-__device__ __forceinline__ void build_dma16(const float* src, float* dst) {
-  const unsigned lds = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_t*)dst)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(lds) : "memory", "m0");
-}
-
-__device__ __forceinline__ void build_stage_rows_async(const float* __restrict__ f, size_t plane, int rows, int cols,
-                                                       int col0, int W, float* lds, int tid, int nthr) {
-  const int nq = cols / 4, n = rows * nq;
-  const int sc = nthr / nq, sq = nthr - sc * nq;
-  int c = tid / nq, q = tid - c * nq;
-  const int wbase = tid & ~(kWave - 1);
-  for (int e0 = 0; e0 < n; e0 += nthr) {
-    const int e = e0 + tid;
-    // a wave whose lanes all lie past the end issues nothing (the lane tail of the last round)
-    if (e < n) {
-      const int col = col0 + 4 * q;
-      const float* src = f + static_cast<size_t>(c) * plane + col;
-      if (col >= 0 && col < W) build_dma16(src, lds + 4 * (e0 + wbase));
-      else *reinterpret_cast<float4*>(lds + 4 * e) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    q += sq;
-    c += sc;
-    if (q >= nq) {
-      q -= nq;
-      ++c;
-    }
-  }
-}
-
-// s_waitcnt vmcnt(63) (expcnt / lgkmcnt untouched): the prefetch issued before a tile's store loop has
-// landed once at most 63 of the wave's younger memory operations -- that loop's >= 64 store
-// instructions -- are still outstanding (launch_build_stem enables the persistent path only when
-// every wave issues all Cs x 4 of them)
-__device__ __forceinline__ void build_wait_prefetch() { __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (15 << 8) | (3 << 14)); }
-
 // LDS image (floats): [A: Cs x WT][Bm: Cs x RS][Wg: Cs x G][invn: G x (WT+RS)][groups: GP x Cg x (WT+RS)]
 __host__ __device__ inline int build_lds_floats(int Cg, int Cs, int WT, int RS, int GP) {
   return Cs * (WT + RS) + Cs * kBuildG + kBuildG * (WT + RS) + GP * Cg * (WT + RS);
 }
 
-// Tile item -> (b, h, column tile, disparity chunk) and the quantities derived from it
-struct BuildTile {
-  int b, h, w0, d0, rs0;
-};
-
-__device__ __forceinline__ BuildTile build_tile(unsigned item, int H, int nwt, int ndc, int WT, int DCH) {
-  BuildTile t;
-  const int dc = item % ndc;
-  const int rest = item / ndc;
-  const int wt = rest % nwt;
-  const int row = rest / nwt;
-  t.b = row / H;
-  t.h = row - t.b * H;
-  t.w0 = wt * WT;
-  t.d0 = dc * DCH;
-  t.rs0 = t.w0 - t.d0 - DCH;                       // first staged R column (a multiple of 4)
-  return t;
-}
-
-// PERSIST: each block walks tiles item0, item0 + gridDim.x, ... (item0 = the XCD remap of its
-// index); before a tile's store loop it issues the NEXT tile's epilogue operands (into the other of
-// two A / Bm buffers) and its first group phase by asynchronous LDS-DMA, so those HBM reads overlap
-// the store stream, and the next tile's norms / dot products overlap the store tail.
-template <int VEC, int GP, bool PERSIST = false>
+template <int VEC, int GP>
 __global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __restrict__ fl,
                                                               const float* __restrict__ fr,
                                                               const float* __restrict__ A,
@@ -364,50 +298,47 @@ __global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __res
                                                               const float* __restrict__ Wg,
                                                               float* __restrict__ out, int C, int Cs, int D,
                                                               int H, int W, int WQ, int DQN, int nwt, int ndc, int dbg,
-                                                              unsigned long long* clk, int ntiles = 0) {
+                                                              unsigned long long* clk) {
   constexpr int G = kBuildG, NPH = G / GP;
-  static_assert(!PERSIST || VEC == 4, "persistent build: 16-B column quads");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Cg = C / G;
   const int WT = 4 * WQ, DCH = 4 * DQN, RS = WT + DCH, NC = WT + RS;
   clock_begin(clk);
-  const unsigned item0 = xcd_remap(blockIdx.x, gridDim.x);
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int dc = item % ndc;
+  const int rest = item / ndc;
+  const int wt = rest % nwt;
+  const int row = rest / nwt;
+  const int b = row / H, h = row - b * H;
+  const int w0 = wt * WT, d0 = dc * DCH;
+  const int rs0 = w0 - d0 - DCH;                   // first staged R column (a multiple of 4)
   const int tid = threadIdx.x, nthr = blockDim.x;
   const bool active = tid < WQ * DQN;
   const int wq = tid % WQ, dq = tid / WQ;
   const size_t plane = static_cast<size_t>(H) * W;
-  float* As0 = smem;
-  float* Bs0 = As0 + Cs * WT;
-  float* Ws = Bs0 + Cs * RS;
+  float* As = smem;
+  float* Bs = As + Cs * WT;
+  float* Ws = Bs + Cs * RS;
   float* invn = Ws + Cs * G;                       // [G][WT + RS] inverse column norms (L then R)
   float* grp = invn + G * NC;                      // [GP][Cg][WT] L rows, then [GP][Cg][RS] R rows
   float* Rg = grp + GP * Cg * WT;
-  float* As1 = Rg + GP * Cg * RS;                  // PERSIST: the second A / Bm buffer
-  float* Bs1 = As1 + Cs * WT;
+  const float* flb = fl + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
+  const float* frb = fr + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
   // R window of this thread: positions base-4 .. base+3 of a staged row, base = 4(wq-dq) + DCH;
   // output (i, j) (d = d0+4dq+i, w = w0+4wq+j) uses position base + j - i = window slot j - i + 4
   const int base = 4 * (wq - dq) + DCH;
+  const int wl0 = w0 + 4 * wq, dl0 = d0 + 4 * dq;
   // dbg bit 2: per-block phase timestamps (wall clock, 100 MHz) of thread 0 into output channel 0
   unsigned long long* ts = reinterpret_cast<unsigned long long*>(out) + static_cast<size_t>(blockIdx.x) * 16;
-  const bool tsr = !PERSIST && (dbg & 4) && tid == 0;
+  const bool tsr = (dbg & 4) && tid == 0;
   if (tsr) ts[0] = wall_clock64();
 
-  const unsigned nt = PERSIST ? static_cast<unsigned>(ntiles) : item0 + 1;
-  BuildTile tl = build_tile(item0, H, nwt, ndc, WT, DCH);
   // epilogue operands travel with the first phase
-  build_stage_rows<VEC>(A + static_cast<size_t>(tl.b) * Cs * plane + static_cast<size_t>(tl.h) * W, plane, Cs, WT,
-                        tl.w0, W, As0, tid, nthr);
-  build_stage_rows<VEC>(Bm + static_cast<size_t>(tl.b) * Cs * plane + static_cast<size_t>(tl.h) * W, plane, Cs, RS,
-                        tl.rs0, W, Bs0, tid, nthr);
+  build_stage_rows<VEC>(A + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W, plane, Cs, WT, w0, W,
+                        As, tid, nthr);
+  build_stage_rows<VEC>(Bm + static_cast<size_t>(b) * Cs * plane + static_cast<size_t>(h) * W, plane, Cs, RS, rs0, W,
+                        Bs, tid, nthr);
   for (int i = tid; i < Cs * G; i += nthr) Ws[i] = Wg[i];
-  // one tile (the whole kernel without PERSIST); `it` counts the block's tiles
-  auto tile = [&](unsigned item, int it) FSMI_BUILD_INL {
-  const int b = tl.b, h = tl.h, w0 = tl.w0, d0 = tl.d0, rs0 = tl.rs0;
-  float* As = (PERSIST && (it & 1)) ? As1 : As0;
-  float* Bs = (PERSIST && (it & 1)) ? Bs1 : Bs0;
-  const float* flb = fl + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
-  const float* frb = fr + static_cast<size_t>(b) * C * plane + static_cast<size_t>(h) * W;
-  const int wl0 = w0 + 4 * wq, dl0 = d0 + 4 * dq;
 
   float gwc[G][4][4];
   const size_t oplane = static_cast<size_t>(D) * plane;
@@ -507,44 +438,18 @@ __global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __res
 #pragma unroll
   for (int ph = 0; ph < NPH; ++ph) {
     if (ph > 0) __syncthreads();                   // previous phase's groups fully consumed
-    if (!PERSIST || it == 0 || ph > 0) {
-      build_stage_rows<VEC>(flb + static_cast<size_t>(ph) * GP * Cg * plane, plane, GP * Cg, WT, w0, W, grp, tid,
-                            nthr);
-      build_stage_rows<VEC>(frb + static_cast<size_t>(ph) * GP * Cg * plane, plane, GP * Cg, RS, rs0, W, Rg, tid,
-                            nthr);
-      __builtin_amdgcn_s_waitcnt(0);               // this thread's LDS-DMA pieces have landed
-      __syncthreads();
-    } else {
-      // phase 0 (and A / Bm) were prefetched before the last tile's stores: wait for them, not for
-      // the stores (__syncthreads()' release fence would wait vmcnt(0)); a bare barrier after the
-      // wave's LDS writes (the zero quads) have completed
-      build_wait_prefetch();
-      __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
-      asm volatile("s_barrier" ::: "memory");
-    }
+    build_stage_rows<VEC>(flb + static_cast<size_t>(ph) * GP * Cg * plane, plane, GP * Cg, WT, w0, W, grp, tid, nthr);
+    build_stage_rows<VEC>(frb + static_cast<size_t>(ph) * GP * Cg * plane, plane, GP * Cg, RS, rs0, W, Rg, tid, nthr);
+    __builtin_amdgcn_s_waitcnt(0);                 // this thread's LDS-DMA pieces have landed
+    __syncthreads();
     if (tsr) ts[1 + 2 * ph] = wall_clock64();
     norms(ph * GP);
     if (active) dots(ph * GP);
     if (tsr) ts[2 + 2 * ph] = wall_clock64();
   }
-  __syncthreads();                                 // invn complete; the group buffers are free
+  __syncthreads();                                 // invn complete
   if (tsr) ts[9] = wall_clock64();
-  if constexpr (PERSIST) {
-    if (item + gridDim.x < nt) {                   // prefetch the next tile while this one stores
-      tl = build_tile(item + gridDim.x, H, nwt, ndc, WT, DCH);
-      float* An = (it & 1) ? As0 : As1;
-      float* Bn = (it & 1) ? Bs0 : Bs1;
-      build_stage_rows_async(A + static_cast<size_t>(tl.b) * Cs * plane + static_cast<size_t>(tl.h) * W, plane, Cs,
-                             WT, tl.w0, W, An, tid, nthr);
-      build_stage_rows_async(Bm + static_cast<size_t>(tl.b) * Cs * plane + static_cast<size_t>(tl.h) * W, plane, Cs,
-                             RS, tl.rs0, W, Bn, tid, nthr);
-      const float* fln = fl + static_cast<size_t>(tl.b) * C * plane + static_cast<size_t>(tl.h) * W;
-      const float* frn = fr + static_cast<size_t>(tl.b) * C * plane + static_cast<size_t>(tl.h) * W;
-      build_stage_rows_async(fln, plane, GP * Cg, WT, tl.w0, W, grp, tid, nthr);
-      build_stage_rows_async(frn, plane, GP * Cg, RS, tl.rs0, W, Rg, tid, nthr);
-    }
-  }
-  if (active) {
+  if (!active) return;
   // normalise: gwc *= inv|L|[w] * inv|R|[w - d]
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -588,14 +493,6 @@ __global__ __launch_bounds__(kThreads) void build_stem_kernel(const float* __res
         }
       }
     }
-  }
-  }  // active
-  };
-  if constexpr (PERSIST) {
-    int it = 0;
-    for (unsigned item = item0; item < nt; item += gridDim.x, ++it) tile(item, it);
-  } else {
-    tile(item0, 0);
   }
   if (tsr) {
     ts[10] = wall_clock64();
@@ -724,69 +621,54 @@ int launch_build_stem(const float* fl, const float* fr, const float* A, const fl
   }
   const int WT = 4 * WQ, DCH = 4 * DQN, RS = WT + DCH;
   const int nthr = (WQ * DQN + kWave - 1) / kWave * kWave;
+  // LDS budget of the image.  One round of tiles (<= 256 blocks, e.g. cfg2's 240): the whole CU,
+  // so the groups take the fewest phases.  More tiles than CUs: at most 80 KB, two blocks per CU, so
+  // one block's stores (the write-dominated half of the kernel) overlap the other's staging and dot
+  // products -- cfg3 (4 pairs, 960 tiles): 0.40 -> 0.47-0.48 of HBM peak, while cfg2 at 80 KB loses
+  // 0.49 -> 0.45.  (A persistent variant -- one block per CU walking its tiles and prefetching the
+  // next tile by LDS-DMA during the current stores -- gained only 0.395 -> 0.402 at cfg3; dropped.)
+  // FSMI_BUILD_LDS_KB overrides the budget (A/B).
+  const int nwt0 = (W + WT - 1) / WT, ndc0 = (D + DCH - 1) / DCH;
+  static const int lds_env = [] {
+    const char* e = std::getenv("FSMI_BUILD_LDS_KB");
+    return e ? std::atoi(e) : 0;
+  }();
+  const size_t lds_cap = static_cast<size_t>(lds_env > 0 && lds_env <= 160 ? lds_env
+                                              : (B * H * nwt0 * ndc0 > 256 ? 80 : 160)) * 1024;
   int GP = kBuildG;
-  while (GP > 1 && static_cast<size_t>(build_lds_floats(Cg, Cs, WT, RS, GP)) * sizeof(float) > 160 * 1024) GP /= 2;
+  while (GP > 1 && static_cast<size_t>(build_lds_floats(Cg, Cs, WT, RS, GP)) * sizeof(float) > lds_cap) GP /= 2;
   const size_t lds = static_cast<size_t>(build_lds_floats(Cg, Cs, WT, RS, GP)) * sizeof(float);
   FSMI_CHECK_ARG(lds <= 160 * 1024, "fsmi_comb_volume_stem: LDS image %zu B too large (C=%d)", lds, C);
   const int nwt = (W + WT - 1) / WT, ndc = (D + DCH - 1) / DCH;
-  const int ntiles = B * H * nwt * ndc;
-  unsigned grid = static_cast<unsigned>(ntiles);
+  const unsigned grid = static_cast<unsigned>(B) * H * nwt * ndc;
   const bool vec = (W % 4) == 0;
   const char* dbs = std::getenv("FSMI_BUILD_DBG");
   const int dbg = dbs ? std::atoi(dbs) : 0;
-  // persistent tiles (build_stem_kernel<.., true>): when the tiles take more than one round of the
-  // 256 CUs (one block each: the LDS image is > 80 KB), each block walks ceil(tiles / 256) of them
-  // and prefetches the next one during the current one's stores.  Needs the second A / Bm buffer to
-  // fit beside the image at the same group phasing, and every wave to issue all Cs x 4 store
-  // instructions of a tile (no ragged column / disparity tiles, no all-idle wave): the prefetch wait
-  // counts on them (build_wait_prefetch).  FSMI_BUILD_PERSIST=0 keeps one tile per block.
-  static const int persist_env = [] {
-    const char* e = std::getenv("FSMI_BUILD_PERSIST");
-    return e ? std::atoi(e) : 1;
-  }();
-  size_t lds_run = lds;
-  bool persist = false;
-  if (persist_env && vec && !dbg && ntiles > 256) {
-    const size_t lds_p = lds + static_cast<size_t>(Cs) * (WT + RS) * sizeof(float);
-    const bool whole = W % WT == 0 && D % DCH == 0 && WQ * DQN > nthr - kWave && Cs * 4 >= 64;
-    if (whole && lds_p <= 160 * 1024) {
-      const int per = (ntiles + 255) / 256;
-      grid = static_cast<unsigned>((ntiles + per - 1) / per);
-      lds_run = lds_p;
-      persist = true;
-    }
-  }
   LaunchTimer t(FSMI_K_COMB, s);
   unsigned long long* clk = clock_slot(FSMI_K_COMB, s, static_cast<long long>(grid) * (nthr / kWave));
-#define FSMI_BUILD_CASE(V, P, PS)                                                                                 \
+#define FSMI_BUILD_CASE(V, P)                                                                                     \
   do {                                                                                                            \
-    const void* fn = reinterpret_cast<const void*>(build_stem_kernel<V, P, PS>);                                  \
-    if (lds_run > 64 * 1024 &&                                                                                    \
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_run)) !=         \
-            hipSuccess)                                                                                           \
+    const void* fn = reinterpret_cast<const void*>(build_stem_kernel<V, P>);                                      \
+    if (lds > 64 * 1024 &&                                                                                        \
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess) \
       return finish_launch("fsmi_comb_volume_stem: LDS attribute");                                               \
     set_replay(FSMI_K_COMB, s, [=] {                                                                              \
-      hipLaunchKernelGGL((build_stem_kernel<V, P, PS>), dim3(grid), dim3(nthr), lds_run, s, fl, fr, A, Bm, Wg, out, \
-                         C, Cs, D, H, W, WQ, DQN, nwt, ndc, dbg, nullptr, ntiles);                                \
+      hipLaunchKernelGGL((build_stem_kernel<V, P>), dim3(grid), dim3(nthr), lds, s, fl, fr, A, Bm, Wg, out, C, Cs,  \
+                         D, H, W, WQ, DQN, nwt, ndc, dbg, nullptr);                                               \
     });                                                                                                           \
-    hipLaunchKernelGGL((build_stem_kernel<V, P, PS>), dim3(grid), dim3(nthr), lds_run, s, fl, fr, A, Bm, Wg, out, C, \
-                       Cs, D, H, W, WQ, DQN, nwt, ndc, dbg, clk, ntiles);                                         \
+    hipLaunchKernelGGL((build_stem_kernel<V, P>), dim3(grid), dim3(nthr), lds, s, fl, fr, A, Bm, Wg, out, C, Cs, D, \
+                       H, W, WQ, DQN, nwt, ndc, dbg, clk);                                                        \
   } while (0)
-  if (persist) {
-    if (GP == 8) FSMI_BUILD_CASE(4, 8, true);
-    else if (GP == 4) FSMI_BUILD_CASE(4, 4, true);
-    else if (GP == 2) FSMI_BUILD_CASE(4, 2, true);
-    else FSMI_BUILD_CASE(4, 1, true);
-  } else if (vec) {
-    if (GP == 8) FSMI_BUILD_CASE(4, 8, false);
-    else if (GP == 4) FSMI_BUILD_CASE(4, 4, false);
-    else if (GP == 2) FSMI_BUILD_CASE(4, 2, false);
-    else FSMI_BUILD_CASE(4, 1, false);
+  if (vec) {
+    if (GP == 8) FSMI_BUILD_CASE(4, 8);
+    else if (GP == 4) FSMI_BUILD_CASE(4, 4);
+    else if (GP == 2) FSMI_BUILD_CASE(4, 2);
+    else FSMI_BUILD_CASE(4, 1);
   } else {
-    if (GP == 8) FSMI_BUILD_CASE(1, 8, false);
-    else if (GP == 4) FSMI_BUILD_CASE(1, 4, false);
-    else if (GP == 2) FSMI_BUILD_CASE(1, 2, false);
-    else FSMI_BUILD_CASE(1, 1, false);
+    if (GP == 8) FSMI_BUILD_CASE(1, 8);
+    else if (GP == 4) FSMI_BUILD_CASE(1, 4);
+    else if (GP == 2) FSMI_BUILD_CASE(1, 2);
+    else FSMI_BUILD_CASE(1, 1);
   }
 #undef FSMI_BUILD_CASE
   return finish_launch("fsmi_comb_volume_stem");

@@ -130,10 +130,10 @@ def test_build_stem_tiles(ops_mod, vit, W, D, tile, monkeypatch):
 
 
 @pytest.mark.parametrize("vit,B,H", [("vits", 1, 135), ("vitl", 2, 150)])
-def test_build_stem_persistent(ops_mod, vit, B, H):
-    """More tiles than one round of the 256 CUs: the persistent build (each block walks several tiles,
-    prefetching the next tile's operands during the current one's stores; 2 and 3 tiles per block,
-    one and two group phases) == the oracle's Conv3d_1x1(cat(gwc, concat(proj(fl), proj(fr))))."""
+def test_build_stem_multiround(ops_mod, vit, B, H):
+    """More tiles than one round of the 256 CUs: the build's 80-KB image (two blocks per CU, the
+    groups staged in four phases instead of one or two) == the oracle's
+    Conv3d_1x1(cat(gwc, concat(proj(fl), proj(fr))))."""
     from foundationstereo_amd.foundation_stereo import FoundationStereo
     W, D = 160, 48
     args = synth.make_args(max_disp=4 * D, corr_levels=2, vit_size=vit)

@@ -42,6 +42,9 @@ ap.add_argument("--out", default="", help="also write the merged table here (e.g
 ap.add_argument("--nosplit", action="store_true", help="also try each shape's current tile without split-K")
 ap.add_argument("--alts-only", action="store_true", help="skip the isolated candidate search (with --nosplit)")
 ap.add_argument("--match", default="", help="regex: only shapes whose key matches")
+ap.add_argument("--prefer-nosplit", type=float, default=-1.0,
+                help="accept an alternative with a smaller split-K factor unless it is slower by more than this "
+                     "relative amount (e.g. 0.002): fewer split-K reduce passes at equal step time")
 ap.add_argument("--try", dest="try_", nargs="*", default=[],
                 help="cfg:nsplit pairs tried in situ on every searched shape they are legal for (e.g. 43:1 43:2)")
 a = ap.parse_args()
@@ -205,7 +208,9 @@ for n, key in enumerate(order):
             continue
         table[key] = {"cfg": c, "nsplit": s, "us": round(best_alone, 1), "insitu": True}
         t = min(evaluate(), evaluate())
-        if t < base * (1 - a.min_gain):
+        cur_split = cur["nsplit"] if cur is not None else 1
+        fewer = a.prefer_nosplit >= 0 and s < cur_split and t < base * (1 + a.prefer_nosplit)
+        if t < base * (1 - a.min_gain) or fewer:
             print(json.dumps({"key": key, "cfg": c, "nsplit": s, "ms": round(t, 3), "was_ms": round(base, 3)}),
                   flush=True)
             base, cur = t, table[key]
