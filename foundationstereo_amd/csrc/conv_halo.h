@@ -16,8 +16,7 @@
 //   * blocks are ordered cout-tile-major over an XCD-aware remap, so each XCD
 //     works on one cout slice and keeps its weights in its 4 MB L2.
 // MFMA v_mfma_f32_32x32x16_f16, three per product (lo*hi, hi*lo, hi*hi), fp32
-// accumulation; fragment maps as in conv2d_x3.hip.  Epilogue identical to
-// fsmi_conv2d (bias, ReLU/GELU, alpha, gamma, residual, channel-offset store).
+// accumulation.  Epilogue: bias, ReLU/GELU, alpha, gamma, residual, channel-offset store.
 //
 // Layout of the sources: this header holds the device code; each (kernel size, 2D / volume)
 // pair compiles in its own translation unit (conv_halo_k{1,3}_{2d,3d}.hip, built in parallel),
