@@ -241,20 +241,13 @@ __global__ __launch_bounds__(256) void volume_pyramid_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------
-// a6: fused lookup.  grid = (ceil(P/64), L, nchunk/4); one wave = 64
-// consecutive pixels x one chunk of kCPC = 4 geo channels (or the corr channel)
-// of one level.  (7 per wave: 36.5 vs 37.4 us alone at cfg2 but 44.2 vs 42.0 us
-// average inside the concurrent loop under rocprof; 2 per wave 37.9 us.)  Coordinates follow bilinear_sampler: x -> 2x/(n-1)-1 -> (x'+1)
-// * ((n-1)/2) (the CPU grid_sampler's align_corners unnormalise), then linear
-// interpolation with zero padding.  The 2r+4 window around floor(x) is loaded
-// once per channel into registers; each tap selects its pair with
-// compile-time indices (no scratch), so a channel costs 2r+4 loads, not 4r+2.
+// a6: fused lookup (core/geometry.py:43-65 + core/utils/utils.py:44-55).  Grid = (B * ceil(HW/64),
+// L, nchunk/4); one wave = 64 consecutive pixels of one image x 4 geo channels (or the corr
+// channel) of one level.  Coordinates follow bilinear_sampler: x -> 2x/(n-1)-1 -> (x'+1) *
+// ((n-1)/2) (the CPU grid_sampler's align_corners unnormalise), then linear interpolation with
+// zero padding.  (2 or 7 channels per wave, FSMI_LOOKUP_CPC: within 1 % back to back and in the
+// step, round 4.)
 // ---------------------------------------------------------------------------
-#ifndef FSMI_LOOKUP_CPC
-#define FSMI_LOOKUP_CPC 4
-#endif
-constexpr int kCPC = FSMI_LOOKUP_CPC;  // geo channels per wave
-
 struct LookupArgs {
   const float* vol[FSMI_MAX_LEVELS];
   const float* cor[FSMI_MAX_LEVELS];
@@ -264,46 +257,150 @@ struct LookupArgs {
   unsigned long long* clk;   // in-kernel launch clock (nullptr: off)
 };
 
-template <int R>
-__global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a) {
+// Branch-free buffer addressing (round 4; replaced per-lane exec-masked global loads and a 64-bit
+// division per lane: 43.9 -> 37.7 us in the cfg2 step, 36.3 -> 30.9 us back to back).
+// Grid = (B * ceil(HW/64), L, nchunk/4): the pixel tile never straddles two images, so b comes
+// from blockIdx.  Every element is a raw buffer load from a per-channel resource (base = the
+// channel's (D_i, HW) plane, wave-uniform, num_records = its size): an element outside [0, D_i)
+// or a lane past the image gets the offset 0x80000000, which the buffer unit answers with 0 without
+// a memory access -- grid_sample's zero padding from the hardware range check, no exec-mask
+// branches.  The offsets are channel-invariant (only the resource base moves), so every channel
+// costs 2r+2 loads + K stores and no address VALU.  Outputs go through the same mechanism
+// (per-channel resource over its K tap planes; tail lanes out of range).
+constexpr unsigned kOOB = 0x80000000u;
+constexpr int kBufFlags = 0x00020000;   // raw buffer, 32-bit data format (gfx9 resource word 3)
+
+// base and size are wave-uniform by construction; readfirstlane states it, so the resource is built
+// in SGPRs (a resource the compiler believes divergent costs a waterfall loop per buffer access)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* base, unsigned bytes) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(base);
+  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v));
+  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v >> 32));
+  float* p = reinterpret_cast<float*>((static_cast<unsigned long long>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, static_cast<int>(__builtin_amdgcn_readfirstlane(bytes)), kBufFlags);
+}
+
+// a kernel-argument array indexed by a uniform level: a select chain keeps the pointer in SGPRs
+// (a dynamic index into the by-value argument copies the array to scratch and makes it divergent)
+__device__ __forceinline__ const float* level_ptr(const float* const (&arr)[FSMI_MAX_LEVELS], int i) {
+  const float* r = arr[0];
+#pragma unroll
+  for (int l = 1; l < FSMI_MAX_LEVELS; ++l) r = i == l ? arr[l] : r;
+  return r;
+}
+
+// Tap interpolation without data-dependent selects (a per-tap select between window elements is
+// folded by the compiler into a dynamically indexed private array: scratch traffic).  A lane's taps
+// sit at window pairs (k + sel, k + sel + 1); sel differs from 1 only where the unnormalise round
+// trip crosses an integer.  FAST (wave-uniform: every lane's every tap at sel = 1): the 2r+2 inner
+// window loads, each tap from fixed window slots.  Otherwise each tap loads its own pair at the
+// element it needs (2 loads per tap, the extra ones served by the caches) -- same products, same
+// add order, same values.
+struct PlaneAddr {          // byte offset of element x of a lane's row: (x * rstride + col) * 4
+  int rstride, col, n;
+  bool live;
+  __device__ __forceinline__ unsigned off(int x) const {
+    return (live && x >= 0 && x < n) ? static_cast<unsigned>(x * rstride + col) * 4u : kOOB;
+  }
+};
+
+template <int R, bool FAST>
+__device__ __forceinline__ void lookup_plane(__amdgpu_buffer_rsrc_t src, const Taps<R>& tp, const PlaneAddr& pa,
+                                             __amdgpu_buffer_rsrc_t dst, const unsigned (&so)[2 * R + 1]) {
+#pragma clang fp contract(off)
   constexpr int K = 2 * R + 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float o[K];
+  if constexpr (FAST) {
+    float win[2 * R + 2];
+#pragma unroll
+    for (int j = 0; j < 2 * R + 2; ++j)
+      win[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src, pa.off(tp.xb + 1 + j), 0, 0));
+#pragma unroll
+    for (int k = 0; k < K; ++k) o[k] = win[k] * (1.f - tp.f[k]) + win[k + 1] * tp.f[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int x0 = tp.xb + k + tp.sel[k];
+      const float v0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src, pa.off(x0), 0, 0));
+      const float v1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src, pa.off(x0 + 1), 0, 0));
+      o[k] = v0 * (1.f - tp.f[k]) + v1 * tp.f[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[k]), dst, so[k], 0, 0);
+}
+
+template <int R, int CPC>
+__global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a, int tiles) {
+  constexpr int K = 2 * R + 1;
+  // the wave index is uniform: readfirstlane tells the compiler, so every resource below stays scalar
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.y;  // level
   clock_begin(a.clk);
   const int chunk = blockIdx.z * 4 + wave;
-  const int nchunk_geo = (a.Cv + kCPC - 1) / kCPC;
-  if (chunk > nchunk_geo) return;
+  const int nchunk_geo = (a.Cv + CPC - 1) / CPC;
+  if (chunk > nchunk_geo) return;                       // wave-uniform
+  const int b = blockIdx.x / tiles;
   const int HW = a.H * a.W;
-  const long long p = static_cast<long long>(blockIdx.x) * 64 + lane;
-  if (p >= static_cast<long long>(a.B) * HW) return;
-  const int b = static_cast<int>(p / HW);
-  const int hw = static_cast<int>(p - static_cast<long long>(b) * HW);
-  const int w = hw % a.W;
-  const float s = static_cast<float>(1 << i);
-  const float ds = a.disp[p] / s;
+  const int hw = (blockIdx.x - b * tiles) * 64 + lane;
+  const bool live = hw < HW;
+  const int hwc = live ? hw : HW - 1;
+  const float inv_s = 1.f / static_cast<float>(1 << i);  // exact: x * 2^-i == x / 2^i
+  const float ds = a.disp[static_cast<size_t>(b) * HW + hwc] * inv_s;
   const int CH = a.L * K * (a.Cv + 1);
-  const int base = i * K * (a.Cv + 1);
-  float* outp = a.out + static_cast<size_t>(b) * CH * HW + hw;
+  const float* outb = a.out + (static_cast<size_t>(b) * CH + static_cast<size_t>(i) * K * (a.Cv + 1)) * HW;
+  unsigned so[K];                                        // store offsets (bytes) in a channel's K planes
+#pragma unroll
+  for (int k = 0; k < K; ++k) so[k] = live ? static_cast<unsigned>(k * HW + hw) * 4u : kOOB;
   Taps<R> tp;
+  PlaneAddr pa;
+  pa.live = live;
+  const float* src_base;
+  unsigned src_bytes;
+  int nplanes, first_plane;
+  size_t src_step;
   if (chunk < nchunk_geo) {
     const int Di = a.D >> i;
     tp.init(ds, Di);
-    const float* vol = a.vol[i] + static_cast<size_t>(b) * a.Cv * Di * HW + hw;
-    const int c0 = chunk * kCPC;
-    if (c0 + kCPC <= a.Cv) {
-#pragma unroll
-      for (int u = 0; u < kCPC; ++u)
-        tp.sample(vol + static_cast<size_t>(c0 + u) * Di * HW, HW, Di,
-                  outp + static_cast<size_t>(base + (c0 + u) * K) * HW, HW);
-    } else {
-      for (int c = c0; c < a.Cv; ++c)
-        tp.sample(vol + static_cast<size_t>(c) * Di * HW, HW, Di, outp + static_cast<size_t>(base + c * K) * HW, HW);
-    }
+    pa.rstride = HW;
+    pa.col = hw;
+    pa.n = Di;
+    const int c0 = chunk * CPC;
+    first_plane = c0;
+    nplanes = min(CPC, a.Cv - c0);
+    src_step = static_cast<size_t>(Di) * HW;
+    src_base = level_ptr(a.vol, i) + (static_cast<size_t>(b) * a.Cv + c0) * src_step;
+    src_bytes = static_cast<unsigned>(Di * HW) * 4u;
   } else {
+    // correlation channel: each lane's row of the W2 pyramid level, contiguous over x
     const int W2i = a.W2 >> i;
-    const float* row = a.cor[i] + static_cast<size_t>(p) * W2i;
-    tp.init(static_cast<float>(w) / s - ds, W2i);
-    tp.sample(row, 1, W2i, outp + static_cast<size_t>(base + a.Cv * K) * HW, HW);
+    const int w = hwc - (hwc / a.W) * a.W;
+    tp.init(static_cast<float>(w) * inv_s - ds, W2i);
+    const int p0 = (blockIdx.x - b * tiles) * 64;        // first pixel of the tile
+    pa.rstride = 1;
+    pa.col = lane * W2i;
+    pa.n = W2i;
+    first_plane = a.Cv;
+    nplanes = 1;
+    src_step = 0;
+    src_base = level_ptr(a.cor, i) + (static_cast<size_t>(b) * HW + p0) * W2i;
+    src_bytes = static_cast<unsigned>(min(64, HW - p0) * W2i) * 4u;
+  }
+  bool odd = false;
+#pragma unroll
+  for (int k = 0; k < K; ++k) odd |= tp.sel[k] != 1;
+  const bool fast = __builtin_amdgcn_ballot_w64(odd) == 0;   // wave-uniform
+#pragma unroll
+  for (int u = 0; u < CPC; ++u) {
+    if (u < nplanes) {                                   // wave-uniform (ragged last chunk)
+      const __amdgpu_buffer_rsrc_t src = buf_rsrc(src_base + u * src_step, src_bytes);
+      const __amdgpu_buffer_rsrc_t dst =
+          buf_rsrc(outb + static_cast<size_t>(first_plane + u) * K * HW, static_cast<unsigned>(K * HW) * 4u);
+      if (fast)
+        lookup_plane<R, true>(src, tp, pa, dst, so);
+      else
+        lookup_plane<R, false>(src, tp, pa, dst, so);
+    }
   }
   clock_end(a.clk);
 }
@@ -408,16 +505,33 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
   a.W = W;
   a.W2 = W2;
   a.B = B;
-  const long long P = static_cast<long long>(B) * H * W;
-  const int nchunk = (Cv + kCPC - 1) / kCPC + 1;
-  dim3 grid(ceil_div(P, 64), num_levels, (nchunk + 3) / 4);
+  const int HW = H * W;
+  const int tiles = (HW + 63) / 64;
+  // buffer offsets inside one channel plane, one channel's K tap planes and one tile's corr rows
+  // are 31-bit
+  FSMI_CHECK_ARG(static_cast<long long>(D) * HW * 4 < (1ll << 31) &&
+                     static_cast<long long>(2 * radius + 1) * HW * 4 < (1ll << 31) &&
+                     static_cast<long long>(B) * tiles < (1ll << 31),
+                 "fsmi_geo_lookup: a channel plane exceeds 2 GB (D=%d, H*W=%d)", D, HW);
+  // geo channels per wave (FSMI_LOOKUP_CPC: 2 / 4 / 7 at radius 4, an A/B knob)
+  static const int env_cpc = [] { const char* e = getenv("FSMI_LOOKUP_CPC"); const int v = e ? atoi(e) : 4;
+                                  return (v == 2 || v == 7) ? v : 4; }();
+  const int cpc = radius == 4 ? env_cpc : 4;
+  const int nchunk = (Cv + cpc - 1) / cpc + 1;
+  dim3 grid(static_cast<unsigned>(B * tiles), num_levels, (nchunk + 3) / 4);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_LOOKUP, s);
-  auto launch = [grid, radius, s](const LookupArgs& la) {
-    switch (radius) {
-      case 2: hipLaunchKernelGGL(geo_lookup_kernel<2>, grid, dim3(256), 0, s, la); break;
-      case 3: hipLaunchKernelGGL(geo_lookup_kernel<3>, grid, dim3(256), 0, s, la); break;
-      default: hipLaunchKernelGGL(geo_lookup_kernel<4>, grid, dim3(256), 0, s, la); break;
+  auto launch = [grid, radius, s, tiles, cpc](const LookupArgs& la) {
+    if (radius == 4 && cpc == 2) {
+      hipLaunchKernelGGL((geo_lookup_kernel<4, 2>), grid, dim3(256), 0, s, la, tiles);
+    } else if (radius == 4 && cpc == 7) {
+      hipLaunchKernelGGL((geo_lookup_kernel<4, 7>), grid, dim3(256), 0, s, la, tiles);
+    } else {
+      switch (radius) {
+        case 2: hipLaunchKernelGGL((geo_lookup_kernel<2, 4>), grid, dim3(256), 0, s, la, tiles); break;
+        case 3: hipLaunchKernelGGL((geo_lookup_kernel<3, 4>), grid, dim3(256), 0, s, la, tiles); break;
+        default: hipLaunchKernelGGL((geo_lookup_kernel<4, 4>), grid, dim3(256), 0, s, la, tiles); break;
+      }
     }
   };
   a.clk = nullptr;

@@ -627,6 +627,26 @@ def test_lookup_vs_oracle(ops_mod, L, D, W):
     close(out, ref(t(disp), coords), atol=1e-5)
 
 
+@pytest.mark.parametrize("B,H,W,D,L", [(2, 3, 37, 48, 4), (3, 5, 64, 24, 2)])
+def test_lookup_batched_ragged(ops_mod, B, H, W, D, L):
+    """Batch > 1 with a pixel count that is not a multiple of 64 (tail lanes, a tile per image) and
+    image 0 at integer disparities everywhere: the round trip puts taps of many lanes at a window
+    pair other than the centre one (the lookup's general tap path), image 1 at fractional ones (its
+    window path); the last image spans the clamped range ends."""
+    from foundationstereo_amd.geometry import Combined_Geo_Encoding_Volume
+    C, Cv = 32, 28
+    f1, f2 = synth.normal(65, (B, C, H, W)), synth.normal(66, (B, C, H, W))
+    vol = synth.normal(67, (B, Cv, D, H, W))
+    disp = synth.uniform(68, (B, 1, H, W), -6.0, D + 6.0)
+    disp[0] = np.round(disp[0])
+    disp[-1, 0, 0, :] = np.linspace(-12.0, D + 12.0, W)
+    ge = Combined_Geo_Encoding_Volume(g(f1), g(f2), g(vol), num_levels=L, dx=torch.linspace(-4, 4, 9))
+    out = ge(g(disp))
+    ref = oracle.GeoEncoding(t(f1), t(f2), t(vol), L, 4)
+    coords = torch.arange(W, dtype=torch.float).view(1, 1, W, 1).repeat(B, H, 1, 1)
+    close(out, ref(t(disp), coords), atol=1e-5)
+
+
 def test_bilinear_sampler_golden(ops_mod, gold):
     from foundationstereo_amd.utils import bilinear_sampler
     close(bilinear_sampler(g(gold["bs_img"]), g(gold["bs_coords"])), gold["bs_out"])
