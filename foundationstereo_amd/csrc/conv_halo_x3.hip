@@ -92,10 +92,11 @@ void split_reduce(const HaloArgs& a, hipStream_t s) {
 
 using namespace fsmi;
 
+// debug phase stamps (fsmi_debug_conv_timestamps): halo convs here, the EdgeNeXt MLP kernel too
+unsigned long long* g_conv_ts = nullptr;
 
 namespace {
 
-unsigned long long* g_conv_ts = nullptr;
 // launches per tile config as launched (0..9 and 11 register / LDS tiles, 10 stride-2, 16 + c K groups,
 // 24..29 pointwise, 30 depth-blocked, 32 + c pipelined): fsmi_conv_launch_counts
 std::atomic<long long> g_cfg_launches[64];

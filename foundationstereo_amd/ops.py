@@ -604,6 +604,28 @@ def dwconv2d(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
+def edgenext_mlp(x: Tensor, res: Tensor, pk1: "PackedConv", bias1: Tensor, pk2: "PackedConv", bias2: Tensor,
+                 gamma: Tensor = None, out: Tensor = None) -> Tensor:
+    """EdgeNextConvEncoder's MLP tail in one kernel (core/submodule.py:583-590):
+    ``res + gamma * pwconv2(gelu(pwconv1(x)))`` over channels at every pixel; ``pk1`` / ``pk2`` the
+    PackedConv of the pwconv1 (E x C) / pwconv2 (C x E) Linear weights as 1x1 convs."""
+    g = _c(gamma.detach().float()) if gamma is not None else None
+    _check("edgenext_mlp", x, res, bias1, bias2, *([g] if g is not None else []))
+    B, C, H, W = x.shape
+    assert res.shape == x.shape, f"edgenext_mlp: res {tuple(res.shape)} vs x {tuple(x.shape)}"
+    assert pk1.k == 1 and pk2.k == 1 and pk1.cin == C and pk2.cout == C and pk2.cin == pk1.cout, \
+        f"edgenext_mlp: W1 {pk1.cout}x{pk1.cin}, W2 {pk2.cout}x{pk2.cin} for {C} channels"
+    x, res = _c(x), _c(res)
+    out = torch.empty_like(x) if out is None else out
+    sb1, sb2 = pk1.scale_bias(bias1), pk2.scale_bias(bias2)
+    _lib.check(_lib.load().fsmi_edgenext_mlp(_p(x), _p(res), _p(out), _p(pk1.whi), _p(pk1.wlo), _p(sb1), _p(pk2.whi),
+                                             _p(pk2.wlo), _p(sb2), _p(g) if g is not None else None, B, C,
+                                             pk1.cout, H, W, _stream(x)), "edgenext_mlp")
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * 2 * C * pk1.cout * B * H * W
+    return out
+
+
 def pool2x(x: Tensor) -> Tensor:
     """``F.avg_pool2d(x, 3, stride=2, padding=1)`` (count_include_pad: every window / 9)."""
     _check("pool2x", x)

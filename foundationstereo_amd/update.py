@@ -93,6 +93,8 @@ def _side_stream(device, idx=0):
 # caller's stream (run_pipelined, whose capture must stay within the box's GPU_MAX_HW_QUEUES = 4
 # streams: a capture spread over more crashed hipGraph instantiation)
 _BRANCH = [1]
+# DispHead's EdgeNeXt MLPs as one fused kernel (ops.edgenext_mlp); FSMI_FUSED_MLP=0: the two 1x1 convs
+_FUSED_MLP = os.environ.get("FSMI_FUSED_MLP", "1") != "0"
 
 
 def _branch_stream(device):
@@ -129,8 +131,14 @@ class DispHead(nn.Module):
         y = _conv(self.conv[0], [_f32(x)], "relu")
         for enc in (self.conv[2], self.conv[3]):
             d = ops.dwconv2d(y, enc.dwconv.weight, enc.dwconv.bias)   # depthwise 7x7; norm=None
-            e = _conv(enc.pwconv1, [d], "gelu")
-            y = _conv(enc.pwconv2, [e], gamma=enc.gamma, res=y)  # x + gamma * pw2(gelu(pw1(.)))
+            if _FUSED_MLP and enc.pwconv1.out_features == 4 * enc.pwconv1.in_features == 512:
+                # x + gamma * pw2(gelu(pw1(.))) in one kernel: the 4C GELU map stays in LDS
+                pk1, b1 = _packed(enc.pwconv1)
+                pk2, b2 = _packed(enc.pwconv2)
+                y = ops.edgenext_mlp(d, y, pk1, b1, pk2, b2, gamma=enc.gamma)
+            else:
+                e = _conv(enc.pwconv1, [d], "gelu")
+                y = _conv(enc.pwconv2, [e], gamma=enc.gamma, res=y)  # x + gamma * pw2(gelu(pw1(.)))
         if res is not None:
             res = res.float()
             if not res.is_contiguous():

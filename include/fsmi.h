@@ -253,6 +253,16 @@ int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* const* whi, con
 
 int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
                   int H, int W, void* stream);
+/* fsmi_edgenext_mlp: the inverted-bottleneck MLP of EdgeNextConvEncoder (core/submodule.py:583-590,
+ *   replacing pwconv1 -> GELU -> pwconv2 -> gamma -> residual):
+ *   out[b,:,p] = res[b,:,p] + gamma * (W2 gelu(W1 x[b,:,p] + b1) + b2), x / res / out (B,C,H,W)
+ *   (out may alias res, not x); w1hi/w1lo = ops.PackedConv of W1 (E x C) as a 1x1 conv,
+ *   sb1 its (2^-wexp, b1) pairs (E float2), w2hi/w2lo / sb2 the same for W2 (C x E); gamma (C) or
+ *   NULL.  Split-precision MFMA (3 fp16 products per MAC) with fp32 accumulation; the 4C hidden
+ *   map stays in LDS.  Built for C = 128, E = 4C (DispHead). */
+int fsmi_edgenext_mlp(const float* x, const float* res, float* out, const void* w1hi, const void* w1lo,
+                      const float* sb1, const void* w2hi, const void* w2lo, const float* sb2, const float* gamma,
+                      int B, int C, int E, int H, int W, void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
  *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */

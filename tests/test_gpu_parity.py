@@ -525,6 +525,38 @@ def test_dwconv2d_vs_torch(ops_mod, KS, shape):
     close(ops_mod.dwconv2d(g(x), g(w), g(b)), ref, atol=1e-5)
 
 
+@pytest.mark.parametrize("B,H,W,gscale", [(1, 120, 160, 1e-6), (2, 7, 13, 0.7), (1, 1, 1, 1.0), (3, 9, 64, 0.3)])
+def test_edgenext_mlp_vs_fp64(ops_mod, B, H, W, gscale):
+    """The fused EdgeNeXt MLP (pwconv1 -> GELU -> pwconv2 -> gamma -> + input, core/submodule.py:583-590)
+    vs the fp64 torch composition: cfg2's shape with the reference's 1e-6 layer-scale init, ragged
+    pixel tiles (91, 1, 576 px per image) with a gamma large enough that the MLP dominates, batch > 1;
+    in place (out = res) as well."""
+    from foundationstereo_amd import update
+    from foundationstereo_amd.submodule import EdgeNextConvEncoder
+    C = 128
+    enc = EdgeNextConvEncoder(C, expan_ratio=4, kernel_size=7, norm=None)
+    synth.init_module_(enc, seed=211)
+    with torch.no_grad():
+        enc.gamma.copy_(torch.from_numpy(synth.uniform(212, (C,), 0.5, 1.5)) * gscale)
+    enc = enc.to(DEV).eval()
+    x = synth.normal(213, (B, C, H, W), 1.5)
+    y = synth.normal(214, (B, C, H, W))
+    with torch.no_grad():
+        pk1, b1 = update._packed(enc.pwconv1)
+        pk2, b2 = update._packed(enc.pwconv2)
+        out = ops_mod.edgenext_mlp(g(x), g(y), pk1, b1, pk2, b2, gamma=enc.gamma)
+        yy = g(y)
+        ops_mod.edgenext_mlp(g(x), yy, pk1, b1, pk2, b2, gamma=enc.gamma, out=yy)
+    P = {k: v.detach().cpu().double() for k, v in enc.state_dict().items()}
+    h = torch.nn.functional.gelu(torch.einsum("ec,bchw->behw", P["pwconv1.weight"], t(x).double())
+                                 + P["pwconv1.bias"].view(1, -1, 1, 1))
+    m = torch.einsum("ce,behw->bchw", P["pwconv2.weight"], h) + P["pwconv2.bias"].view(1, -1, 1, 1)
+    ref = t(y).double() + P["gamma"].view(1, -1, 1, 1) * m
+    tol = 2e-5 * max(1.0, float(m.abs().max()) * gscale)
+    close(out, ref, atol=tol, rtol=1e-5)
+    close(yy, out, atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("shape", [(1, 128, 60, 80), (2, 3, 7, 9), (1, 2, 1, 1), (1, 4, 30, 40)])
 def test_pool2x_vs_torch(ops_mod, shape):
     """pool2x (avg 3x3, stride 2, pad 1, count_include_pad) vs the torch CPU fp32 op."""

@@ -150,3 +150,37 @@ def test_conv_tuning_db_wellformed():
                 or (e["cfg"] == 30 and kd == 17 and ks == 1)
                 or 34 <= e["cfg"] <= 41 or (e["cfg"] in (11, 43) and kd == 1 and D == 1)) \
             and 1 <= e["nsplit"] <= 8, (key, e)
+
+
+def test_gelu_erf_coefficients_accuracy():
+    """The branch-free erf of the GELU epilogues (csrc/conv_halo.h erf_nb), its coefficients read
+    from the header and evaluated as the device does (fmaf Horner in float32, select at |z| = 1):
+    within 3 ulp of math.erf over [-6, 6] (tools/fit_erf.py fits them)."""
+    import math
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "foundationstereo_amd", "csrc", "conv_halo.h")).read()
+    body = src[src.index("float erf_nb(float z)"):src.index("__device__ __forceinline__ float gelu_erf_h")]
+    num = r"(-?\d\.\d+e[+-]\d+)f"
+    p = [float(re.search(r"float p = " + num, body).group(1))] + \
+        [float(v) for v in re.findall(r"p = fmaf\(p, t, " + num + r"\)", body)]
+    r = [float(re.search(r"float r = " + num, body).group(1))] + \
+        [float(v) for v in re.findall(r"r = fmaf\(r, az, " + num + r"\)", body)]
+    assert len(p) == 7 and len(r) == 11
+    f32 = np.float32
+
+    def horner(c, x):
+        acc = np.full_like(x, f32(c[0]))
+        for ci in c[1:]:
+            acc = (acc.astype(np.float64) * x + f32(ci)).astype(f32)
+        return acc
+
+    z = np.linspace(-6, 6, 400001).astype(f32)
+    t = (z * z).astype(f32)
+    small = (z.astype(np.float64) * horner(p, t)).astype(f32)
+    az = np.minimum(np.abs(z), f32(4))
+    e = np.exp2(-(t * f32(1.4426950408889634)).astype(f32).astype(np.float64)).astype(f32)
+    big = np.copysign((1.0 - e.astype(np.float64) * horner(r, az)).astype(f32), z)
+    got = np.where(np.abs(z) < 1, small, big).astype(np.float64)
+    ref = np.array([math.erf(float(v)) for v in z])
+    ulp = np.spacing(np.abs(ref).astype(f32)).astype(np.float64)
+    assert (np.abs(got - ref) / ulp).max() < 3.0
