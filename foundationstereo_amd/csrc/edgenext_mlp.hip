@@ -15,6 +15,9 @@
 //     tile into a second, 4C-wide hi / lo image that overwrites the first (same LDS);
 //   * GEMM 2: 8 waves x (32 out x 32 px), K = 4C, two accumulators per wave (even / odd k-steps)
 //     so consecutive MFMAs are independent; epilogue res + gamma * (v + b2), stored once.
+// One block of 8 waves per CU (139 KB of LDS).  A 4-wave variant staging the hidden map a quarter at
+// a time (75 KB, two blocks per CU) was faster alone (40 vs 50 us at cfg2) but slower in the step
+// (48.0-48.6 vs 47.8 ms): its longer-lived blocks hold CUs the concurrent streams' convs need.
 // HBM traffic per pixel: x, res and out, C floats each -- the hidden map never leaves the CU.
 // Weights: the halo kernels' pre-split packing (ops.PackedConv, [cin chunk][cout][32] hi / lo, rows
 // scaled by 2^wexp[co] with (2^-wexp, bias) pairs), read from L2 one chunk ahead.
@@ -106,11 +109,12 @@ __global__ __launch_bounds__(512) void edgenext_mlp_kernel(MlpArgs a) {
 #pragma unroll
   for (int u = 0; u < XT; ++u) {
     const int task = u * 512 + tid, px = task % PX, g = task / PX;
-    const bool ok = p0 + px < HW;
-    const float* src = a.x + (static_cast<size_t>(b) * C + 8 * g) * HW + p0 + px;
+    const bool ok = p0 + px < HW;        // tail pixels load the last one (no branch) and drop it
+    const float* src = a.x + (static_cast<size_t>(b) * C + 8 * g) * HW + min(p0 + px, static_cast<int>(HW) - 1);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      xv[u][t] = ok ? src[static_cast<size_t>(t) * HW] : 0.f;
+      const float v = src[static_cast<size_t>(t) * HW];
+      xv[u][t] = ok ? v : 0.f;
       mx = fmaxf(mx, fabsf(xv[u][t]));
     }
   }
