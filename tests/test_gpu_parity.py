@@ -514,9 +514,10 @@ def test_context_blocks_vs_torch(ops_mod):
 
 
 @pytest.mark.parametrize("KS,shape", [(7, (2, 5, 19, 70)), (7, (1, 3, 120, 160)), (3, (1, 4, 17, 9)),
-                                      (5, (1, 2, 33, 65))])
+                                      (5, (1, 2, 33, 65)), (7, (2, 3, 37, 100)), (5, (1, 2, 9, 4))])
 def test_dwconv2d_vs_torch(ops_mod, KS, shape):
-    """Depthwise conv (EdgeNeXt dwconv) vs the fp64 torch conv; ragged tiles, 1e-5 abs (49-term fp32 sums)."""
+    """Depthwise conv (EdgeNeXt dwconv) vs the fp64 torch conv; ragged tiles, 1e-5 abs (49-term fp32 sums);
+    W % 4 == 0 shapes take the float4 staging (incl. ragged rows / a partial last column tile)."""
     C = shape[1]
     x = synth.normal(201, shape)
     w = synth.normal(202, (C, 1, KS, KS), 0.2)
