@@ -22,8 +22,6 @@
 #define FSMI_PW_TWOBAR 0                           // 1: the round-2 schedule (a second barrier per chunk)
 #endif
 
-// dma16 writes m0 (the LDS-DMA base): nothing else in these kernels uses it
-#pragma clang diagnostic ignored "-Winline-asm"
 
 namespace fsmi {
 namespace {
@@ -42,10 +40,16 @@ __device__ __forceinline__ void wait_lgkm0() {     // lgkmcnt = 0, vmcnt / expcn
 // One LDS-DMA wave instruction: 16 B per lane from src to LDS dst + 16 * lane (dst wave-uniform).
 // Inline asm, so the compiler neither counts it nor guards the ring's LDS reads with its own
 // vmcnt(0) (it cannot tell the ring slots apart); every wait on it is explicit (wait_vmcnt).
+// M0 is compiler-reserved (an "m0" clobber is ignored), so the statement saves and restores it, and
+// the M0 write -> LDS-DMA hazard needs one wait state (s_nop 0) inside the string.  Without both,
+// a DMA could use a stale M0 (another ring slot) or leave the compiler's M0 clobbered: rare wrong
+// partial sums in the split-K pointwise tests (round 4: 1 of ~40 runs; fixed here).
 __device__ __forceinline__ void dma16(const float* src, float* dst) {
   typedef __attribute__((address_space(3))) float lds_float;
   const unsigned lds = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(reinterpret_cast<size_t>((lds_float*)dst)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(lds) : "memory", "m0");
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
 }
 
 // a bare workgroup barrier: __syncthreads()' release fence would wait for vmcnt(0), i.e. for

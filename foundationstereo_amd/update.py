@@ -93,6 +93,9 @@ def _side_stream(device, idx=0):
 # caller's stream (run_pipelined, whose capture must stay within the box's GPU_MAX_HW_QUEUES = 4
 # streams: a capture spread over more crashed hipGraph instantiation)
 _BRANCH = [1]
+# run_pipelined: gru08(t+1)'s interp(gru16(t+1)) enqueued right after gru16(t+1), beside gru04(t)
+# (FSMI_EARLY_INTERP=0: after gru04(t), as the reference orders it)
+EARLY_INTERP = os.environ.get("FSMI_EARLY_INTERP", "1") != "0"
 # DispHead's EdgeNeXt MLPs as one fused kernel (ops.edgenext_mlp); FSMI_FUSED_MLP=0: the two 1x1 convs
 _FUSED_MLP = os.environ.get("FSMI_FUSED_MLP", "1") != "0"
 
@@ -453,15 +456,20 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru16(t+1), beside gru04(t)
                     n2 = self.gru16(att[2], n2, inp[2], pool2x(n1))
+                    # gru08(t+1)'s upsampled gru16 input, also beside gru04(t): one kernel less between
+                    # gru04(t) and gru08(t+1)
+                    up2 = interp(n2, n1) if EARLY_INTERP else None
                 _BRANCH[0] = 1
             _BRANCH[0] = 1 if main_branch else 0
             n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0))
             _BRANCH[0] = 1
             if t + 1 < iters:
                 s_gru.wait_stream(main)                  # gru04(t)
+                # both branches in order: forking gru08's 1x1 branch to the (then idle) branch stream
+                # crashed the process under capture (segfault, round 4)
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru08(t+1), beside the heads + motion(t+1)
-                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1))
+                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
                 _BRANCH[0] = 1
             if t + 1 == iters:
                 # test mode upsamples only the last iteration's disparity: the reference computes the
