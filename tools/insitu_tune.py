@@ -203,9 +203,10 @@ for n, key in enumerate(order):
     print(f"[insitu] {n + 1}/{len(order)} {key} x{counts[key]}: alternatives {alts}, step {base:.3f} ms "
           f"({(time.time() - t_start) / 60:.1f} min)", file=sys.stderr, flush=True)
     for (c, s) in alts:
-        eff = cur["nsplit"] if cur is None or cur.get("insitu") or not ops._SPLIT_CAP else min(cur["nsplit"], ops._SPLIT_CAP)
-        if cur is not None and cur["cfg"] == c and eff == s:
-            continue
+        if cur is not None:
+            eff = cur["nsplit"] if cur.get("insitu") or not ops._SPLIT_CAP else min(cur["nsplit"], ops._SPLIT_CAP)
+            if cur["cfg"] == c and eff == s:
+                continue
         table[key] = {"cfg": c, "nsplit": s, "us": round(best_alone, 1), "insitu": True}
         t = min(evaluate(), evaluate())
         cur_split = cur["nsplit"] if cur is not None else 1
