@@ -112,6 +112,11 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) wrow[i] = min(m0 + (wm * TM + i) * 32 + rl, a.CoutP - 1) * HKC + 8 * hsel;
   half8 wf[2][TM][2][2];                           // [buffer][i][k half][hi, lo]
+  // global loads one load_wf issues: the explicit vmcnt waits below count them.  The one-product
+  // build loads no lo halves -- left to the compiler, the unused lo loads were dropped and the
+  // waits, still counting 4 * TM, let a chunk's LDS-DMA be read before it landed (round 4: garbage
+  // in convc1's output in the fast build, one run in three)
+  constexpr int WLD = (FSMI_NPROD == 3 ? 4 : 2) * TM;
   auto load_wf = [&](auto buf_c, int c) FSMI_HALO_INL {
     constexpr int buf = decltype(buf_c)::value;
     const size_t base = static_cast<size_t>(c) * a.CoutP * HKC;
@@ -120,7 +125,8 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         wf[buf][i][k][0] = *reinterpret_cast<const half8*>(a.whi + base + wrow[i] + 16 * k);
-        wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+        if constexpr (FSMI_NPROD == 3) wf[buf][i][k][1] = *reinterpret_cast<const half8*>(a.wlo + base + wrow[i] + 16 * k);
+        else wf[buf][i][k][1] = wf[buf][i][k][0];
       }
   };
 
@@ -146,20 +152,20 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
     for (int s = 0; s < NS - 1; ++s) dma(min(c_begin + s, c_end - 1), s);
   }
   // chunk q (buffer parity P): prefetch weights q+1 and chunk q+NS-1, wait for chunk q and
-  // weights q (the 2*OPS + 4*TM younger memory ops may stay in flight), barrier, MFMAs, barrier
+  // weights q (the 2*OPS + WLD younger memory ops may stay in flight), barrier, MFMAs, barrier
   auto step = [&](auto par_c, int q) FSMI_HALO_INL {
     constexpr int P = decltype(par_c)::value;
     const int c = c_begin + q;
     load_wf(std::integral_constant<int, P ^ 1>(), min(c + 1, c_end - 1));
 #if FSMI_PW_TWOBAR
     dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
-    wait_vmcnt<2 * OPS + 4 * TM>();                // this wave's part of chunk q has landed
+    wait_vmcnt<2 * OPS + WLD>();                   // this wave's part of chunk q has landed
     bar();                                         // ... and every wave's
 #else
     // one barrier per chunk: chunk q's DMA is waited for (chunks q+1 .. q+NS-2 and the weights just
     // issued may stay in flight), the barrier makes every wave's part visible AND retires every
     // wave's reads of chunk q-1's slot, which chunk q+NS-1 then refills
-    wait_vmcnt<(NS - 2) * OPS + 4 * TM>();
+    wait_vmcnt<(NS - 2) * OPS + WLD>();
     bar();
     dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
 #endif

@@ -450,10 +450,18 @@ _GATE_MODE = {"zr": 0, "blend_small": 1, "blend_large": 2}
 _RANGE_DEBUG = os.environ.get("FSMI_RANGE_DEBUG", "0") == "1"   # diagnostics: sync + check after each conv
 
 
-def _range_debug(what, segs):
-    if _RANGE_DEBUG and not torch.cuda.is_current_stream_capturing() and range_overflowed(reset=True):
+def _range_debug(what, segs, out=None, ch=None):
+    if not _RANGE_DEBUG or torch.cuda.is_current_stream_capturing():
+        return
+    if range_overflowed(reset=True):
         desc = [(tuple(t.shape), c0, n, float(t[:, c0:c0 + n].abs().max())) for t, c0, n in segs]
         print(f"[fsmi range] {what}: segments (shape, c0, n, max|x|) {desc}", flush=True)
+    if out is not None:                  # an output far beyond any activation: report its producer
+        o = out if ch is None else out[:, ch[0]:ch[1]]
+        m = float(o.abs().max())
+        if not m < 1e15:
+            desc = [(tuple(t.shape), c0, n, float(t[:, c0:c0 + n].abs().max())) for t, c0, n in segs]
+            print(f"[fsmi range] {what}: OUTPUT max|y| {m:.3g}; inputs {desc}", flush=True)
 
 
 def conv2d_gate(segs, pk, bias: Tensor, mode: str, h: Tensor, z: Tensor, att: Tensor = None, rh: Tensor = None,
@@ -586,7 +594,7 @@ def conv2d(segs, pk, bias: Tensor = None, act=None, alpha: float = 1.0, gamma: T
         _p(gamma) if gamma is not None else None, _p(res) if res is not None else None,
         res.shape[1] if res is not None else 0, _p(out), out.shape[1], co0, B, pk.cout, pk.k, H, W, ACT[act],
         float(alpha), tcfg, nsplit, _p(ws), ws.numel(), stream), "conv2d_halo_x3")
-    _range_debug(f"conv2d k{pk.k} {cin}->{pk.cout}", norm)
+    _range_debug(f"conv2d k{pk.k} {cin}->{pk.cout}", norm, out, (co0, co0 + pk.cout))
     del keep
     return out
 
