@@ -21,6 +21,9 @@
 #ifndef FSMI_PW_TWOBAR
 #define FSMI_PW_TWOBAR 0                           // 1: the round-2 schedule (a second barrier per chunk)
 #endif
+#ifndef FSMI_PW_WLD_ADJ
+#define FSMI_PW_WLD_ADJ 0
+#endif
 
 
 namespace fsmi {
@@ -116,7 +119,8 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
   // build loads no lo halves -- left to the compiler, the unused lo loads were dropped and the
   // waits, still counting 4 * TM, let a chunk's LDS-DMA be read before it landed (round 4: garbage
   // in convc1's output in the fast build, one run in three)
-  constexpr int WLD = (FSMI_NPROD == 3 ? 4 : 2) * TM;
+  // (FSMI_PW_WLD_ADJ: a deliberately wrong count, only for tests/test_dma_waits.py's negative build)
+  constexpr int WLD = (FSMI_NPROD == 3 ? 4 : 2) * TM + FSMI_PW_WLD_ADJ;
   auto load_wf = [&](auto buf_c, int c) FSMI_HALO_INL {
     constexpr int buf = decltype(buf_c)::value;
     const size_t base = static_cast<size_t>(c) * a.CoutP * HKC;
@@ -145,27 +149,27 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
   float scale = 1.f;
   int sx = kNoExp;
   bool ovf = false;
-  // prologue: weights of the first chunk, then NS - 1 chunks in flight
-  if (n > 0) {
-    load_wf(std::integral_constant<int, 0>(), c_begin);
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s) dma(min(c_begin + s, c_end - 1), s);
-  }
   // chunk q (buffer parity P): prefetch weights q+1 and chunk q+NS-1, wait for chunk q and
-  // weights q (the 2*OPS + WLD younger memory ops may stay in flight), barrier, MFMAs, barrier
-  auto step = [&](auto par_c, int q) FSMI_HALO_INL {
+  // weights q (the 2*OPS + WLD younger memory ops may stay in flight), barrier, MFMAs, barrier.
+  // LAST (the odd tail step, q = n - 1): its weight prefetch would be dead code -- the compiler
+  // drops it -- so it issues none and its wait counts none.  The n == 1 tail follows the prologue
+  // directly, with only the (NS - 2) clamped DMA groups after chunk 0's; the static check
+  // (tests/test_dma_waits.py) found the round-4 tail waiting for WLD loads that did not exist there.
+  auto step = [&](auto par_c, auto last_c, int q) FSMI_HALO_INL {
     constexpr int P = decltype(par_c)::value;
+    constexpr bool LAST = decltype(last_c)::value;
+    constexpr int W = LAST ? 0 : WLD;
     const int c = c_begin + q;
-    load_wf(std::integral_constant<int, P ^ 1>(), min(c + 1, c_end - 1));
+    if constexpr (!LAST) load_wf(std::integral_constant<int, P ^ 1>(), min(c + 1, c_end - 1));
 #if FSMI_PW_TWOBAR
     dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
-    wait_vmcnt<2 * OPS + WLD>();                   // this wave's part of chunk q has landed
+    wait_vmcnt<2 * OPS + W>();                     // this wave's part of chunk q has landed
     bar();                                         // ... and every wave's
 #else
     // one barrier per chunk: chunk q's DMA is waited for (chunks q+1 .. q+NS-2 and the weights just
     // issued may stay in flight), the barrier makes every wave's part visible AND retires every
     // wave's reads of chunk q-1's slot, which chunk q+NS-1 then refills
-    wait_vmcnt<(NS - 2) * OPS + WLD>();
+    wait_vmcnt<(NS - 2) * OPS + W>();
     bar();
     dma(min(c + NS - 1, c_end - 1), (q + NS - 1) % NS);
 #endif
@@ -254,12 +258,20 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
     bar();                                         // every wave is done with slot q % NS
 #endif
   };
-  int q = 0;
-  for (; q + 1 < n; q += 2) {
-    step(std::integral_constant<int, 0>(), q);
-    step(std::integral_constant<int, 1>(), q + 1);
+  // prologue: weights of the first chunk, then NS - 1 chunks in flight; the chunk loop sits inside
+  // the same branch, so every path to a ring wait passes the prologue's DMAs
+  if (n > 0) {
+    load_wf(std::integral_constant<int, 0>(), c_begin);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) dma(min(c_begin + s, c_end - 1), s);
+    using F = std::false_type;
+    int q = 0;
+    for (; q + 1 < n; q += 2) {
+      step(std::integral_constant<int, 0>(), F(), q);
+      step(std::integral_constant<int, 1>(), F(), q + 1);
+    }
+    if (q < n) step(std::integral_constant<int, 0>(), std::true_type(), q);
   }
-  if (q < n) step(std::integral_constant<int, 0>(), q);
   wait_vmcnt<0>();                                 // the tail's clamped prefetches land before exit
   flag_overflow(a, ovf);
 
