@@ -38,6 +38,8 @@ from foundationstereo_amd import synth  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, B/s (MI355X_MICROARCH.md chip table)
 MFMA_F16_PEAK = 2.5e15  # dense fp16 MFMA, FLOP/s (MI355X_MICROARCH.md; no sparsity)
+MFMA_F32_PEAK = 157.3e12  # f32-input MFMA (v_mfma_f32_32x32x2_f32), FLOP/s (MI355X_MICROARCH.md)
+GEO_KERNELS = ("comb", "norm", "corr", "volpyr", "lookup")   # instrumented with the in-kernel clock
 
 # BASELINE.json configs (name -> H, W, max_disp, iters, vit, pairs per GPU)
 CONFIGS = {
@@ -74,6 +76,23 @@ def build_bytes(B, C, H4, W4, D4, Cs=28):
     return 4 * B * N * (2 * C + 2 * Cs + Cs * D4)
 
 
+def allpairs_bytes(B, C, H4, W4, L):
+    """All-pairs correlation pyramid: read fl, fr once, write the L levels (B,H4,W4,W4>>i)."""
+    N = H4 * W4
+    return 4 * B * (2 * C * N + sum(N * (W4 >> i) for i in range(L)))
+
+
+def allpairs_flops(B, C, H4, W4):
+    """The dense feature x feature contraction: 2*C multiply-adds per (w1, w2) pair of every row."""
+    return 2 * B * C * H4 * W4 * W4
+
+
+def volpyr_bytes(B, Cv, D4, H4, W4, L):
+    """Filtered-volume pyramid: read level 0, write levels 1..L-1."""
+    N = H4 * W4
+    return 4 * B * N * Cv * (D4 + sum(D4 >> i for i in range(1, L)))
+
+
 def make_model(args, device, rank):
     from foundationstereo_amd.foundation_stereo import FoundationStereo
     m = FoundationStereo(args).eval()
@@ -84,31 +103,43 @@ def make_model(args, device, rank):
     return m
 
 
-def cpu_baseline(args, H, W, iters, threads, hiera=False):
-    """Time the CPU oracle on one pair of the same workload on the host cores."""
+def cpu_baseline(args, H, W, iters, threads, hiera=False, pair=0):
+    """Time the CPU oracle on one pair of the same workload on the host cores: global pair ``pair``
+    of the bench's batch (images and backbone features seeded 0x5EED + pair, as the ranks make them)."""
     import oracle
     torch.set_num_threads(threads)
     from foundationstereo_amd.foundation_stereo import FoundationStereo
     m = FoundationStereo(args)
     synth.init_module_(m, seed=1234)
     P = {k: v.float() if v.is_floating_point() else v for k, v in m.state_dict().items()}
-    left, right = synth.stereo_images(1, H, W)
+    seed = 0x5EED + pair
+    left, right = synth.stereo_images(1, H, W, seed=seed)
     T = oracle.StageTimer()
     t0 = time.perf_counter()
     with torch.no_grad():
         if hiera:
             def features(B, h, w):
-                fl, fr, vf = synth.backbone_features(B, h, w, args.vit_size, shift_px=8)
+                fl, fr, vf = synth.backbone_features(B, h, w, args.vit_size, seed=seed, shift_px=8)
                 return [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr], torch.from_numpy(vf)
             out = oracle.oracle_hierarchical(P, args, torch.from_numpy(left), torch.from_numpy(right), features,
                                        iters=iters, timer=T)
         else:
-            fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, shift_px=8)
+            fl, fr, vf = synth.backbone_features(1, H, W, args.vit_size, seed=seed, shift_px=8)
             out = oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
                                   [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr],
                                   torch.from_numpy(vf), iters=iters, timer=T)
     dt = time.perf_counter() - t0
     return dt, T.stages, out
+
+
+def parity_block(out, refs, vs):
+    """``parity`` of the line: max |dd| of the gathered output's pairs ``refs`` (global pair index ->
+    the oracle's disparity for it) -- at N > 1 pair 0 (rank 0's) and the last pair (the last rank's,
+    through the all-gather)."""
+    per = {int(i): float((out[i].float().cpu() - r.float()).abs().max()) for i, r in refs.items()}
+    dd = max(per.values())
+    return {"max_abs_dd_px": dd, "vs": vs, "pairs_checked": sorted(per), "per_pair_dd_px": per,
+            "tolerance_px": 1e-3, "ok": dd < 1e-3}
 
 
 def _cpu_model():
@@ -180,9 +211,12 @@ def dist_selftest(a):
         elapsed = float(t.item())
     ok = bool(torch.allclose(out, (full[:, 0] - full[:, 1]).abs().mean(1, keepdim=True)))
     if rank == 0:
+        ref = (full[:, 0] - full[:, 1]).abs().mean(1, keepdim=True)
+        parity = parity_block(out, {0: ref[0], B - 1: ref[B - 1]} if world > 1 else {0: ref[0]},
+                              "the stand-in function on the host")
         print(json.dumps({"metric": "dist self-test (no model)", "value": a.steps * B / elapsed, "unit": "pairs/s",
                           "n_gpus": wsz, "world_size": wsz, "backend": backend, "steps": a.steps,
-                          "warmup": a.warmup, "gathered_ok": ok,
+                          "warmup": a.warmup, "gathered_ok": ok, "parity": parity,
                           "data": "dist self-test: stand-in per-pair function on CPU tensors, not a measurement"}),
               flush=True)
     if world > 1:
@@ -315,7 +349,9 @@ def main():
     # output (the captured forward's last node, ops.range_poison_); both are reported
     range_overflow = ops.range_overflowed(reset=False)
     out_finite = bool(torch.isfinite(out).all())
-    lk_step_ms, lk_step_n = ops.timer_query_clock("lookup") if a.graph else (0.0, 0)
+    # the timed step's own launches (the last replay), by the kernels' clocks baked into the graph
+    in_step = {k: ops.timer_query_clock(k, captured=True) for k in GEO_KERNELS} if a.graph else {}
+    lk_step_ms, lk_step_n = in_step.get("lookup", (0.0, 0))
     if a.graph:
         # graph replays carry no per-kernel events (HIP rejects external event nodes during
         # capture): time the kernels over one eager pass of the identical step instead, on one
@@ -336,6 +372,9 @@ def main():
     lk_ev_ms, cb_ev_ms = lk_ms, cb_ms
     lk_ck_ms, lk_ck_n = ops.timer_query_clock("lookup")
     cb_ck_ms, cb_ck_n = ops.timer_query_clock("comb")
+    eager_clock = {k: ops.timer_query_clock(k) for k in GEO_KERNELS}
+    if not a.graph:
+        in_step = eager_clock
     cv_flops = ops.conv_flops()
     range_overflow_eager = ops.range_overflowed(reset=True)   # the timing pass after the timed region
     # roofline durations, each the live measurement that agrees with rocprof's per-launch average
@@ -359,10 +398,26 @@ def main():
     # algorithmic bytes per launch, averaged over the passes (one size unless hierarchical)
     lk_bytes = sum(lookup_bytes(bl, ph // 4, pw // 4, 28, L, args.corr_radius) for ph, pw in sizes) / len(sizes)
     cb_bytes = build_bytes(bl, C, sizes[-1][0] // 4, sizes[-1][1] // 4, D4)   # the replayed (last) launch
+    # per forward (every pass), the algorithmic bytes / flops of each geometry kernel
+    fwd_bytes = {
+        "comb": sum(build_bytes(bl, C, ph // 4, pw // 4, D4) for ph, pw in sizes),
+        "corr": sum(allpairs_bytes(bl, C, ph // 4, pw // 4, L) for ph, pw in sizes),   # norm + corr together
+        "volpyr": sum(volpyr_bytes(bl, 28, D4, ph // 4, pw // 4, L) for ph, pw in sizes),
+        "lookup": iters * sum(lookup_bytes(bl, ph // 4, pw // 4, 28, L, args.corr_radius) for ph, pw in sizes),
+    }
+    corr_flops = sum(allpairs_flops(bl, C, ph // 4, pw // 4) for ph, pw in sizes)
+    step_ms = {k: v[0] for k, v in in_step.items()}
+    step_n = {k: v[1] for k, v in in_step.items()}
+    geo_ms = sum(step_ms.get(k, 0.0) for k in GEO_KERNELS)
+    geo_bytes = sum(fwd_bytes.values())
+    geo_complete = all(step_n.get(k, 0) > 0 for k in GEO_KERNELS) and step_n.get("lookup") == iters * len(sizes)
     lk_avg = lk_rep / 1e3 if lk_rep else (lk_ms / 1e3) / max(lk_n, 1)
     lk_head_in_step = bool(lk_in_step)
     lk_head = lk_in_step / 1e3 if lk_in_step else lk_avg          # seconds per launch, headline
-    cb_avg = cb_rep / 1e3 if cb_rep else (cb_ms / 1e3) / max(cb_n, 1)
+    cb_avg = cb_rep / 1e3 if cb_rep else (cb_ms / 1e3) / max(cb_n, 1)     # back-to-back replays (secondary)
+    cb_in_step = step_ms.get("comb", 0.0) / 1e3 / step_n["comb"] if step_n.get("comb") else None
+    cb_head = cb_in_step or cb_avg
+    cb_head_bytes = fwd_bytes["comb"] / len(sizes) if cb_in_step else cb_bytes
     traffic = traffic_build = None
     pmc_path = os.path.join(REPO, "profiles", f"pmc_lookup_summary_{a.config}.json")
     if not os.path.exists(pmc_path):
@@ -438,30 +493,62 @@ def main():
                                "peak": MFMA_F16_PEAK / nprod / 1e12, "unit": "TFLOP/s",
                                "frac": cv_flops / (elapsed / a.steps) / (MFMA_F16_PEAK / nprod) if cv_n else None,
                                "timed_over": "timed region (whole step)"},
-        "roofline_build": {"kernel": "comb_volume_stem", "bound": "hbm",
-                           "achieved": cb_bytes / cb_avg / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
-                           "unit": "GB/s", "frac": cb_bytes / cb_avg / HBM_PEAK if cb_n else None,
+        # the single-pass cost-volume build INSIDE the timed step (its in-kernel clock baked into the
+        # graph, like the lookup's); the back-to-back replay of one launch (MALL-warm) is secondary
+        "roofline_build": {"kernel": "build_stem_kernel (gwc + concat + corr_stem[0])", "bound": "hbm",
+                           "achieved": cb_head_bytes / cb_head / 1e9 if cb_n else None, "peak": HBM_PEAK / 1e9,
+                           "unit": "GB/s", "frac": cb_head_bytes / cb_head / HBM_PEAK if cb_n else None,
                            "traffic": traffic_build,
-                           "algorithmic_bytes": cb_bytes, "avg_us": cb_avg * 1e6,
-                           "timed_by": f"hip events over {REPS} back-to-back replays of the step's launch",
-                           "avg_us_events": cb_ev_ms * 1e3 / max(cb_n, 1),
-                           "avg_us_kernel_clock": cb_ck_ms * 1e3 / max(cb_ck_n, 1), "launches": cb_n},
+                           "algorithmic_bytes": cb_head_bytes, "avg_us": cb_head * 1e6,
+                           "timed_over": "the timed step (last replay's launch)" if cb_in_step else "replays",
+                           "timed_by": "in-kernel clock (s_memrealtime per wave) in the captured graph" if cb_in_step
+                                       else f"hip events over {REPS} back-to-back replays of the step's launch",
+                           "avg_us_replay": cb_avg * 1e6, "frac_replay": cb_bytes / cb_avg / HBM_PEAK if cb_n else None,
+                           "avg_us_events_single_stream": cb_ev_ms * 1e3 / max(cb_n, 1),
+                           "avg_us_kernel_clock_single_stream": cb_ck_ms * 1e3 / max(cb_ck_n, 1), "launches": cb_n},
+        # north star: build + correlation lookup as ONE per-pair figure -- every geometry kernel of the
+        # timed step (build, all-pairs normalisation + MFMA pass, volume pyramid, the `iters` lookups)
+        # by its in-step clock, against their algorithmic bytes (5.78 GB per cfg2 pair, L=4)
+        "roofline_build_lookup": {
+            "kernels": "build_stem + normalize_cols + allpairs_corr + volume_pyramid + geo_lookup x iters",
+            "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK / 1e9,
+            "achieved": geo_bytes / (geo_ms / 1e3) / 1e9 if geo_complete else None,
+            "frac": geo_bytes / (geo_ms / 1e3) / HBM_PEAK if geo_complete else None,
+            "algorithmic_bytes_per_pair": geo_bytes / bl, "us_per_pair": geo_ms * 1e3 / bl,
+            "timed_over": "the timed step (last replay)" if a.graph else "eager step",
+            "per_kernel_us": {k: round(step_ms.get(k, 0.0) * 1e3, 2) for k in GEO_KERNELS},
+            "per_kernel_launches": step_n,
+            "per_kernel_bytes": fwd_bytes},
+        # the one dense contraction north_star puts on MFMA: the all-pairs correlation (fp32 MFMA)
+        "allpairs_mfma": {"kernel": "allpairs_corr_direct_kernel (v_mfma_f32_32x32x2_f32)", "bound": "mfma",
+                          "flops": corr_flops, "unit": "TFLOP/s", "peak": MFMA_F32_PEAK / 1e12,
+                          "avg_us": step_ms.get("corr", 0.0) * 1e3 / max(step_n.get("corr", 0), 1),
+                          "achieved": (corr_flops / (step_ms["corr"] / 1e3) / 1e12) if step_n.get("corr") else None,
+                          "frac": (corr_flops / (step_ms["corr"] / 1e3) / MFMA_F32_PEAK) if step_n.get("corr") else None,
+                          "normalize_us": step_ms.get("norm", 0.0) * 1e3 / max(step_n.get("norm", 0), 1),
+                          "timed_over": "the timed step (last replay)" if a.graph else "eager step"},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and (world > 1 or not a.no_cpu_baseline):
         # the host cores this process is given: OMP_NUM_THREADS (16 on the GPU box = its CPU share
         # per GPU; os.cpu_count() there reports the whole machine, shared with other jobs)
         threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1)
         dt, stages, ref = cpu_baseline(args, H, W, iters, threads, hiera=a.config in HIERA)
-        # the oracle ran pair 0 of this very workload (same seeds): the step's own disparity vs it
-        dd = float((out[0].float().cpu() - ref[0].float()).abs().max())
-        res["parity"] = {"max_abs_dd_px": dd, "vs": "CPU oracle (fp32), pair 0 of the timed step's output",
-                         "tolerance_px": 1e-3, "ok": dd < 1e-3}
+        # the oracle ran pair 0 of this very workload (same seeds): the step's own disparity vs it; at
+        # N > 1 also the batch's last pair, computed by the last rank and returned by the all-gather
+        # (a multi-GPU line always carries parity; --no-cpu-baseline skips it at N = 1 only)
+        refs = {0: ref[0]}
+        if world > 1 and B > 1:
+            refs[B - 1] = cpu_baseline(args, H, W, iters, threads, hiera=a.config in HIERA, pair=B - 1)[2][0]
+        res["parity"] = parity_block(out, refs, "CPU oracle (fp32), the timed step's gathered output")
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = {"value": 1.0 / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
                                "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
                                "sample": f"1 pair of {a.config} (all {iters} iterations) through the fp32 "
                                          f"torch-CPU oracle, {dt:.1f} s",
                                "stages_s": {k: round(v, 3) for k, v in stages.items()}}
     if rank == 0:
+        # a multi-GPU line never prints without parity (its pairs came back through the all-gather)
+        assert world == 1 or "max_abs_dd_px" in res.get("parity", {}), "multi-GPU line without parity"
         print(json.dumps(res), flush=True)
     if not out_finite:
         raise SystemExit("bench.py: the timed step returned non-finite disparities (range overflow)")

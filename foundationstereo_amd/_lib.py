@@ -28,6 +28,7 @@ SIGNATURES = {
     "fsmi_allpairs_corr": [_P, _P, _PP, _I, _I, _I, _I, _I, _P, _P],
     "fsmi_volume_pyramid": [_P, _PP, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_geo_lookup": [_PP, _PP, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_geo_lookup_coords": [_PP, _PP, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_bilinear_sampler_1d": [_P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_disparity_regression": [_P, _P, _I, _I, _I, _I, _P],
     "fsmi_softmax_regression": [_P, _P, _I, _I, _I, _I, _P],
@@ -65,10 +66,12 @@ SIGNATURES = {
     "fsmi_timer_query": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
     "fsmi_timer_query_clock": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
     "fsmi_timer_replay": [_I, _I, ctypes.POINTER(ctypes.c_double)],
+    "fsmi_timer_query_clock_captured": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
+    "fsmi_timer_release_captured": [],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
-           "gru_reset", "gru_blend", "conv3d", "conv2d", "dwconv", "resize", "dt"]
+           "gru_reset", "gru_blend", "conv3d", "conv2d", "dwconv", "resize", "dt", "norm"]
 
 _lib = None
 

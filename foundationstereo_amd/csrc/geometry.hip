@@ -127,7 +127,9 @@ __device__ __forceinline__ void corr_epilogue(const f32x16& acc, float* __restri
 // per pixel: out[b,c,p] = f[b,c,p] / max(||f[b,:,p]||_2, 1e-12).  grid.y picks fl / fr.
 __global__ __launch_bounds__(256) void normalize_cols_kernel(const float* __restrict__ f0,
                                                              const float* __restrict__ f1, float* __restrict__ o0,
-                                                             float* __restrict__ o1, int C, int HW, long long P) {
+                                                             float* __restrict__ o1, int C, int HW, long long P,
+                                                             unsigned long long* clk) {
+  clock_begin(clk);
   const long long p = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
   if (p >= P) return;
   const float* f = blockIdx.y ? f1 : f0;
@@ -156,6 +158,7 @@ __global__ __launch_bounds__(256) void normalize_cols_kernel(const float* __rest
     for (int u = 0; u < 8; ++u) o[base + static_cast<size_t>(c + u) * HW] = v[u] / n;
   }
   for (; c < C; ++c) o[base + static_cast<size_t>(c) * HW] = f[base + static_cast<size_t>(c) * HW] / n;
+  clock_end(clk);
 }
 
 // all-pairs on pre-normalised operands: no LDS, no barriers.  Block = (b, h,
@@ -164,7 +167,8 @@ __global__ __launch_bounds__(256) void normalize_cols_kernel(const float* __rest
 // of the MFMAs that consume them.
 __global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_direct_kernel(
     const float* __restrict__ nl, const float* __restrict__ nr, float* __restrict__ lv0, float* __restrict__ lv1,
-    float* __restrict__ lv2, float* __restrict__ lv3, int L, int C, int H, int W, int T) {
+    float* __restrict__ lv2, float* __restrict__ lv3, int L, int C, int H, int W, int T, unsigned long long* clk) {
+  clock_begin(clk);
   const int lane = threadIdx.x & 63, t2 = threadIdx.x >> 6;
   const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
   const int row = item / T, t1 = item - row * T;
@@ -197,6 +201,7 @@ __global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_direct_kernel
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb, acc, 0, 0, 0);
   }
   corr_epilogue(acc, lv0, lv1, lv2, lv3, L, H, W, b, h, t1, t2, lane);
+  clock_end(clk);
 }
 
 // ---------------------------------------------------------------------------
@@ -208,7 +213,9 @@ __global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_direct_kernel
 template <int S>
 __global__ __launch_bounds__(256) void volume_pyramid_kernel(const float* __restrict__ vol, float* __restrict__ o1,
                                                              float* __restrict__ o2, float* __restrict__ o3, int D,
-                                                             int HW, int nq, long long total) {
+                                                             int HW, int nq, long long total,
+                                                             unsigned long long* clk) {
+  clock_begin(clk);
   const long long idx = blockIdx.x * 256ll + threadIdx.x;
   if (idx >= total) return;
   const int p = static_cast<int>(idx % HW);
@@ -238,6 +245,7 @@ __global__ __launch_bounds__(256) void volume_pyramid_kernel(const float* __rest
     }
   }
   (void)len;
+  clock_end(clk);
 }
 
 // ---------------------------------------------------------------------------
@@ -252,6 +260,7 @@ struct LookupArgs {
   const float* vol[FSMI_MAX_LEVELS];
   const float* cor[FSMI_MAX_LEVELS];
   const float* disp;
+  const float* coords;       // (B,H,W) column coordinates of the corr taps; nullptr: the pixel column w
   float* out;
   int L, Cv, D, H, W, W2, B;
   unsigned long long* clk;   // in-kernel launch clock (nullptr: off)
@@ -374,8 +383,11 @@ __global__ __launch_bounds__(256) void geo_lookup_kernel(LookupArgs a, int tiles
   } else {
     // correlation channel: each lane's row of the W2 pyramid level, contiguous over x
     const int W2i = a.W2 >> i;
+    // the reference's init_x0 = coords / 2^i - disp / 2^i + dx (core/geometry.py:57); the model passes
+    // coords = arange(W) per row (core/foundation_stereo.py:231), derived here without a load
     const int w = hwc - (hwc / a.W) * a.W;
-    tp.init(static_cast<float>(w) * inv_s - ds, W2i);
+    const float cw = a.coords ? a.coords[static_cast<size_t>(b) * HW + hwc] : static_cast<float>(w);
+    tp.init(cw * inv_s - ds, W2i);
     const int p0 = (blockIdx.x - b * tiles) * 64;        // first pixel of the tile
     pa.rstride = 1;
     pa.col = lane * W2i;
@@ -449,9 +461,11 @@ int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, i
     const long long P = static_cast<long long>(B) * H * W;
     float* nl = ws;
     float* nr = ws + static_cast<size_t>(B) * C * H * W;
-    hipLaunchKernelGGL(normalize_cols_kernel, dim3(ceil_div(P, 64), 2), dim3(64), 0, s, fl, fr, nl, nr, C, H * W, P);
-    hipLaunchKernelGGL(allpairs_corr_direct_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
-                       nl, nr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);
+    const unsigned ngrid = ceil_div(P, 64), cgrid = static_cast<unsigned>(B) * H * T;
+    hipLaunchKernelGGL(normalize_cols_kernel, dim3(ngrid, 2), dim3(64), 0, s, fl, fr, nl, nr, C, H * W, P,
+                       clock_slot(FSMI_K_NORM, s, 2ll * ngrid));
+    hipLaunchKernelGGL(allpairs_corr_direct_kernel, dim3(cgrid), dim3(T * kWave), 0, s, nl, nr, lv[0], lv[1], lv[2],
+                       lv[3], num_levels, C, H, W, T, clock_slot(FSMI_K_CORR, s, static_cast<long long>(cgrid) * T));
   } else {
     hipLaunchKernelGGL(allpairs_corr_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
                        fl, fr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);
@@ -474,16 +488,24 @@ int fsmi_volume_pyramid(const float* vol, float* const* levels, int num_levels, 
   const unsigned grid = ceil_div(total, 256);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_VOLPYR, s);
+  unsigned long long* clk = clock_slot(FSMI_K_VOLPYR, s, 4ll * grid);
   switch (S) {
-    case 2: hipLaunchKernelGGL(volume_pyramid_kernel<2>, dim3(grid), dim3(256), 0, s, vol, o[0], o[1], o[2], D, HW, nq, total); break;
-    case 4: hipLaunchKernelGGL(volume_pyramid_kernel<4>, dim3(grid), dim3(256), 0, s, vol, o[0], o[1], o[2], D, HW, nq, total); break;
-    default: hipLaunchKernelGGL(volume_pyramid_kernel<8>, dim3(grid), dim3(256), 0, s, vol, o[0], o[1], o[2], D, HW, nq, total); break;
+    case 2: hipLaunchKernelGGL(volume_pyramid_kernel<2>, dim3(grid), dim3(256), 0, s, vol, o[0], o[1], o[2], D, HW, nq, total, clk); break;
+    case 4: hipLaunchKernelGGL(volume_pyramid_kernel<4>, dim3(grid), dim3(256), 0, s, vol, o[0], o[1], o[2], D, HW, nq, total, clk); break;
+    default: hipLaunchKernelGGL(volume_pyramid_kernel<8>, dim3(grid), dim3(256), 0, s, vol, o[0], o[1], o[2], D, HW, nq, total, clk); break;
   }
   return finish_launch("fsmi_volume_pyramid");
 }
 
 int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_levels, const float* disp, float* out,
                     int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2, void* stream) {
+  return fsmi_geo_lookup_coords(vol_levels, corr_levels, disp, nullptr, out, num_levels, radius, B, Cv, D, H, W, W2,
+                                stream);
+}
+
+int fsmi_geo_lookup_coords(const float* const* vol_levels, const float* const* corr_levels, const float* disp,
+                           const float* coords, float* out, int num_levels, int radius, int B, int Cv, int D, int H,
+                           int W, int W2, void* stream) {
   FSMI_CHECK_ARG(vol_levels && corr_levels && disp && out, "fsmi_geo_lookup: null pointer");
   FSMI_CHECK_ARG(num_levels >= 1 && num_levels <= FSMI_MAX_LEVELS, "fsmi_geo_lookup: num_levels %d", num_levels);
   FSMI_CHECK_ARG(radius == 4 || radius == 2 || radius == 3, "fsmi_geo_lookup: radius %d unsupported", radius);
@@ -497,6 +519,7 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
     if (i < num_levels) FSMI_CHECK_ARG(a.vol[i] && a.cor[i], "fsmi_geo_lookup: null level %d", i);
   }
   a.disp = disp;
+  a.coords = coords;
   a.out = out;
   a.L = num_levels;
   a.Cv = Cv;

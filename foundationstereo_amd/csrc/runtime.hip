@@ -58,7 +58,13 @@ size_t g_clock_top = 0;
 // process: the graph keeps writing them on every replay, so a later session (clock_init) must never
 // hand the same addresses to new launches.  Sessions bump-allocate above this floor.
 size_t g_clock_floor = 0;
+// (offset, nwaves) per instrumented launch: eager launches of the current session (cleared by
+// clock_init), and launches baked into captured graphs (kept across sessions, like their slots, until
+// fsmi_timer_release_captured -- the graphs keep rewriting them on every replay)
 std::vector<std::pair<size_t, long long>> g_clock_launch[FSMI_K_COUNT];
+std::vector<std::pair<size_t, long long>> g_clock_captured[FSMI_K_COUNT];
+// launches that found the arena full, eager (this session) and captured (reported by the queries)
+long long g_clock_dropped[FSMI_K_COUNT], g_clock_dropped_cap[FSMI_K_COUNT];
 
 static int clock_init() {
   if (!g_clock && hipMalloc(&g_clock, sizeof(unsigned long long) * kClockArena) != hipSuccess) {
@@ -70,6 +76,7 @@ static int clock_init() {
     return FSMI_ERR_ARG;
   g_clock_top = g_clock_floor;
   for (auto& v : g_clock_launch) v.clear();
+  for (auto& d : g_clock_dropped) d = 0;
   return FSMI_OK;
 }
 
@@ -82,11 +89,16 @@ unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves)
   if (st != hipStreamCaptureStatusNone && !g_clock_in_capture) return nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
   const size_t need = 2 * static_cast<size_t>(nwaves);
-  if (g_clock_top + need > kClockArena) return nullptr;
-  g_clock_launch[kernel].emplace_back(g_clock_top, nwaves);
+  const bool captured = st != hipStreamCaptureStatusNone;
+  if (g_clock_top + need > kClockArena) {
+    // the query of this kernel fails instead of silently under-counting
+    ++(captured ? g_clock_dropped_cap : g_clock_dropped)[kernel];
+    return nullptr;
+  }
+  (captured ? g_clock_captured : g_clock_launch)[kernel].emplace_back(g_clock_top, nwaves);
   unsigned long long* p = g_clock + g_clock_top;
   g_clock_top += need;
-  if (st != hipStreamCaptureStatusNone) g_clock_floor = g_clock_top;   // baked into a graph: reserved
+  if (captured) g_clock_floor = g_clock_top;   // baked into a graph: reserved
   return p;
 }
 
@@ -271,10 +283,8 @@ int fsmi_get_range_safe(int* safe) {
   return FSMI_OK;
 }
 
-int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count) {
-  FSMI_CHECK_ARG(kernel >= 0 && kernel < FSMI_K_COUNT, "fsmi_timer_query_clock: bad kernel id %d", kernel);
-  std::lock_guard<std::mutex> lk(fsmi::g_mu);
-  const auto& launches = fsmi::g_clock_launch[kernel];
+static int query_clock(const std::vector<std::pair<size_t, long long>>& launches, double* total_ms,
+                       long long* count) {
   double tot = 0.0;
   long long n = 0;
   if (!launches.empty()) {
@@ -302,6 +312,31 @@ int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count) {
   }
   if (total_ms) *total_ms = tot;
   if (count) *count = n;
+  return FSMI_OK;
+}
+
+int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count) {
+  FSMI_CHECK_ARG(kernel >= 0 && kernel < FSMI_K_COUNT, "fsmi_timer_query_clock: bad kernel id %d", kernel);
+  std::lock_guard<std::mutex> lk(fsmi::g_mu);
+  FSMI_CHECK_ARG(fsmi::g_clock_dropped[kernel] == 0, "fsmi_timer_query_clock: %lld launches of kernel %d found the "
+                 "clock arena full", fsmi::g_clock_dropped[kernel], kernel);
+  return query_clock(fsmi::g_clock_launch[kernel], total_ms, count);
+}
+
+int fsmi_timer_query_clock_captured(int kernel, double* total_ms, long long* count) {
+  FSMI_CHECK_ARG(kernel >= 0 && kernel < FSMI_K_COUNT, "fsmi_timer_query_clock_captured: bad kernel id %d", kernel);
+  std::lock_guard<std::mutex> lk(fsmi::g_mu);
+  FSMI_CHECK_ARG(fsmi::g_clock_dropped_cap[kernel] == 0, "fsmi_timer_query_clock_captured: %lld captured launches "
+                 "of kernel %d found the clock arena full", fsmi::g_clock_dropped_cap[kernel], kernel);
+  return query_clock(fsmi::g_clock_captured[kernel], total_ms, count);
+}
+
+int fsmi_timer_release_captured(void) {
+  std::lock_guard<std::mutex> lk(fsmi::g_mu);
+  for (auto& v : fsmi::g_clock_captured) v.clear();
+  for (auto& d : fsmi::g_clock_dropped_cap) d = 0;
+  fsmi::g_clock_floor = 0;
+  fsmi::g_clock_top = 0;
   return FSMI_OK;
 }
 

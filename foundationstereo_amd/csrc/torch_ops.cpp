@@ -107,7 +107,8 @@ std::vector<Tensor> volume_pyramid(const Tensor& vol_, int64_t num_levels) {
   return levels;
 }
 
-Tensor geo_lookup(at::TensorList vol_levels, at::TensorList corr_levels, const Tensor& disp_, int64_t radius) {
+Tensor geo_lookup(at::TensorList vol_levels, at::TensorList corr_levels, const Tensor& disp_, int64_t radius,
+                  const c10::optional<Tensor>& coords_) {
   const int64_t L = vol_levels.size();
   TORCH_CHECK(L >= 1 && L <= 8 && (int64_t)corr_levels.size() == L, "geo_lookup: 1..8 levels of each pyramid");
   check_dev("geo_lookup", disp_);
@@ -131,7 +132,14 @@ Tensor geo_lookup(at::TensorList vol_levels, at::TensorList corr_levels, const T
   Tensor disp = dense(disp_);
   const int64_t K = 2 * radius + 1;
   Tensor out = at::empty({B, L * K * (Cv + 1), H, W}, disp.options());
-  ok(fsmi_geo_lookup(pv.data(), pc.data(), cp(disp), mp(out), L, radius, B, Cv, D, H, W, W2, stream_of(disp)),
+  Tensor coords;       // the reference's coords (core/geometry.py:57): any layout of B*H*W values
+  if (coords_.has_value() && coords_->defined()) {
+    check_dev("geo_lookup", *coords_);
+    TORCH_CHECK(coords_->numel() == B * H * W, "geo_lookup: coords must hold B*H*W values");
+    coords = dense(coords_->reshape({B, H, W}));
+  }
+  ok(fsmi_geo_lookup_coords(pv.data(), pc.data(), cp(disp), coords.defined() ? cp(coords) : nullptr, mp(out), L,
+                            radius, B, Cv, D, H, W, W2, stream_of(disp)),
      "geo_lookup");
   return out;
 }
@@ -204,7 +212,7 @@ TORCH_LIBRARY(fsmi, m) {
   m.def("allpairs_corr(Tensor fl, Tensor fr, int num_levels) -> Tensor[]");
   // level 0 IS `vol` (the reference keeps the filtered volume as its level 0, core/geometry.py:29-36)
   m.def("volume_pyramid(Tensor(a -> *) vol, int num_levels) -> Tensor(a)[]");
-  m.def("geo_lookup(Tensor[] vol_levels, Tensor[] corr_levels, Tensor disp, int radius) -> Tensor");
+  m.def("geo_lookup(Tensor[] vol_levels, Tensor[] corr_levels, Tensor disp, int radius, Tensor? coords=None) -> Tensor");
   m.def("bilinear_sampler_1d(Tensor img, Tensor x) -> Tensor");
   m.def("disparity_regression(Tensor prob, int maxdisp) -> Tensor");
   m.def("softmax_regression(Tensor logits) -> Tensor");

@@ -329,7 +329,18 @@ class FoundationStereo(nn.Module):
         with autocast(mp, md):
             features_left, features_right, vit_feat = self._backbone(image1, image2)
             ctx_s = None
-            if _update.OVERLAP and CTX_OVERLAP and image1.is_cuda and not torch.is_grad_enabled():
+            ctx_overlap = _update.OVERLAP and CTX_OVERLAP and image1.is_cuda and not torch.is_grad_enabled()
+            corr_pyr = None
+            if ctx_overlap:
+                # the two HBM / MFMA kernels the north star measures run ALONE on the chip, before any
+                # side stream forks: the cost-volume build, then the all-pairs correlation pyramid (it
+                # needs only the features; the side streams' convs used to stretch it 10x beside the
+                # classifier).  ~70 us on the main stream; the side streams are far off the critical path
+                vol = self.build_stem_volume(features_left[0], features_right[0])
+                corr_pyr = Combined_Geo_Encoding_Volume.corr_pyramid(features_left[0].float(),
+                                                                     features_right[0].float(),
+                                                                     self.args.corr_levels)
+            if ctx_overlap:
                 # stem_2 + context net + CAM / SAM read only the images and vit_feat: a side stream
                 # runs them beside the volume build and the 3D filtering (joined before the loop)
                 main = torch.cuda.current_stream(image1.device)
@@ -351,7 +362,8 @@ class FoundationStereo(nn.Module):
                         self.cost_agg.gate_logits(features_left)
                     g_ev = torch.cuda.Event()
                     g_ev.record(g_s)
-            vol = self.build_stem_volume(features_left[0], features_right[0])
+            if not ctx_overlap:
+                vol = self.build_stem_volume(features_left[0], features_right[0])
             if fuse:
                 # corr_feature_att's sigmoid(gate) * vol in the last ResNet block's epilogue; the gates
                 # are joined right before it (~1 ms of volume convs after the fork)
@@ -367,13 +379,13 @@ class FoundationStereo(nn.Module):
                 vol = self.corr_feature_att(self.corr_stem[1:](vol), features_left[0])
             vol = self.cost_agg(vol, features_left, gates=None if gates is None else gates[1:])
             geo_fn = None
-            if ctx_s is not None:
-                # the geometry pyramids (all-pairs correlation + volume pyramid) beside the classifier
-                geo_s = _update._side_stream(image1.device, 1)
-                geo_s.wait_stream(main)
-                with torch.cuda.stream(geo_s):
-                    geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(),
-                                                          vol.float(), num_levels=self.args.corr_levels, dx=self.dx)
+            if corr_pyr is not None:
+                # the volume pyramid (HBM-bound) on the main stream right after the hourglass, before the
+                # classifier's convs start: the gate and disparity-transformer branches joined inside the
+                # hourglass and the context stream (~1/10 of the hourglass's work) has long finished
+                geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(),
+                                                      vol.float(), num_levels=self.args.corr_levels, dx=self.dx,
+                                                      init_corr_pyramid=corr_pyr)
             if init_disp is None:
                 cl = self.classifier
                 head = cl[2]   # Conv3d(14, 1, 7, padding=3): direct gfx950 kernel (MIOpen: ~1 TFLOP/s here)
@@ -388,10 +400,6 @@ class FoundationStereo(nn.Module):
         if geo_fn is None:
             geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
                                                   num_levels=self.args.corr_levels, dx=self.dx)
-        else:
-            main.wait_stream(geo_s)
-            for t in [*geo_fn.init_corr_pyramid, *geo_fn.geo_volume_pyramid]:
-                t.record_stream(main)
         disp = init_disp.float()
         disp_preds = []
         disp_up = None

@@ -17,7 +17,10 @@ from . import ops
 
 
 class Combined_Geo_Encoding_Volume:
-    def __init__(self, init_fmap1, init_fmap2, geo_volume, num_levels=2, dx=None):
+    def __init__(self, init_fmap1, init_fmap2, geo_volume, num_levels=2, dx=None, *, init_corr_pyramid=None):
+        """core/geometry.py:9-40.  ``init_corr_pyramid``: the all-pairs pyramid of the same features,
+        already computed (``corr_pyramid``; FoundationStereo.forward runs it right after the cost
+        volume, alone on the chip, long before the filtered volume exists)."""
         self.num_levels = num_levels
         self.dx = dx
         self.radius = 4 if dx is None else (int(dx.numel()) - 1) // 2
@@ -32,18 +35,33 @@ class Combined_Geo_Encoding_Volume:
             ref = torch.linspace(-self.radius, self.radius, 2 * self.radius + 1)
             if not torch.equal(dx.detach().float().reshape(-1).cpu(), ref):
                 raise ValueError("fsmi geo lookup supports dx = linspace(-r, r, 2r+1) only")
-        self.init_corr_pyramid = ops.allpairs_corr(fl, fr, num_levels)
+        if init_corr_pyramid is not None:
+            assert len(init_corr_pyramid) == num_levels and init_corr_pyramid[0].shape == (B, H, W, W), \
+                "init_corr_pyramid does not match the features"
+            self.init_corr_pyramid = list(init_corr_pyramid)
+        else:
+            self.init_corr_pyramid = self.corr_pyramid(fl, fr, num_levels)
         self.geo_volume_pyramid = ops.volume_pyramid(vol, num_levels)
         self.shape = (B, C, D, H, W)
 
     def __call__(self, disp, coords=None, low_memory=False, out=None):
         """Per-iteration lookup (core/geometry.py:43-65).
 
-        ``coords`` must be the pixel column index ``arange(W)`` as the reference
-        builds it (core/foundation_stereo.py:231); the kernel derives it from
-        the pixel position instead of reading it.
+        ``coords``: the left-image column of each pixel, any layout of B*H*W values (the reference's
+        (B,H,W,1), core/foundation_stereo.py:231); the correlation taps sit at coords/2^i - disp/2^i + k
+        exactly as the reference's ``init_x0`` (:57).  ``None`` -- what this package's forward passes --
+        lets the kernel derive the column from the pixel index instead of loading it (the reference's
+        own coords are that arange(W)).
         """
-        return ops.geo_lookup(self.geo_volume_pyramid, self.init_corr_pyramid, disp.float(), self.radius, out=out)
+        if coords is not None:
+            coords = coords.float()
+        return ops.geo_lookup(self.geo_volume_pyramid, self.init_corr_pyramid, disp.float(), self.radius, out=out,
+                              coords=coords)
+
+    @staticmethod
+    def corr_pyramid(fmap1, fmap2, num_levels):
+        """core/geometry.py:24-40 on HIP: [(B,H,W,W>>i)], the avg-pool pyramid of ``corr``."""
+        return ops.allpairs_corr(fmap1.float(), fmap2.float(), num_levels)
 
     @staticmethod
     def corr(fmap1, fmap2):

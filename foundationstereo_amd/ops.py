@@ -49,6 +49,16 @@ def _p(t: Tensor) -> int:
     return t.data_ptr()
 
 
+def _overlaps(a: Tensor, b: Tensor) -> bool:
+    """Whether the byte ranges a and b span on the same device intersect."""
+    if a.device != b.device or a.numel() == 0 or b.numel() == 0:
+        return False
+    a0, b0 = a.data_ptr(), b.data_ptr()
+    a1 = a0 + (sum((n - 1) * st for n, st in zip(a.shape, a.stride())) + 1) * a.element_size()
+    b1 = b0 + (sum((n - 1) * st for n, st in zip(b.shape, b.stride())) + 1) * b.element_size()
+    return a0 < b1 and b0 < a1
+
+
 # ---------------------------------------------------------------- cost volume
 
 def gwc_volume(fl: Tensor, fr: Tensor, maxdisp: int, num_groups: int) -> Tensor:
@@ -142,9 +152,11 @@ def volume_pyramid(vol: Tensor, num_levels: int) -> List[Tensor]:
 
 
 def geo_lookup(vol_levels: Sequence[Tensor], corr_levels: Sequence[Tensor], disp: Tensor, radius: int,
-               out: Tensor = None) -> Tensor:
-    """core/geometry.py:43-65 -> (B, L*(2r+1)*(Cv+1), H, W)."""
-    _check("geo_lookup", disp, *vol_levels, *corr_levels)
+               out: Tensor = None, coords: Tensor = None) -> Tensor:
+    """core/geometry.py:43-65 -> (B, L*(2r+1)*(Cv+1), H, W).  ``coords``: the reference's column
+    coordinates (any layout with B*H*W elements, e.g. its (B,H,W,1)); None = the pixel column w, which
+    is what the reference passes (core/foundation_stereo.py:231)."""
+    _check("geo_lookup", disp, *vol_levels, *corr_levels, *([coords] if coords is not None else []))
     L = len(vol_levels)
     B, Cv, D, H, W = vol_levels[0].shape
     W2 = corr_levels[0].shape[-1]
@@ -153,15 +165,19 @@ def geo_lookup(vol_levels: Sequence[Tensor], corr_levels: Sequence[Tensor], disp
         assert vol_levels[i].shape == (B, Cv, D >> i, H, W) and vol_levels[i].is_contiguous()
         assert corr_levels[i].shape == (B, H, W, W2 >> i) and corr_levels[i].is_contiguous()
     disp = _c(disp)
+    if coords is not None:
+        assert coords.numel() == B * H * W, f"coords {tuple(coords.shape)}: expected B*H*W = {B * H * W} values"
+        coords = _c(coords.reshape(B, H, W))
     K = 2 * radius + 1
     if out is None:
         out = torch.empty((B, L * K * (Cv + 1), H, W), device=disp.device, dtype=torch.float32)
     pv, kv = _lib.ptr_array([_p(t) for t in vol_levels])
     pc, kc = _lib.ptr_array([_p(t) for t in corr_levels])
-    _lib.check(_lib.load().fsmi_geo_lookup(pv, pc, _p(disp), _p(out), L, radius, B, Cv, D, H, W, W2,
-                                           _stream(disp)), "geo_lookup")
+    _lib.check(_lib.load().fsmi_geo_lookup_coords(pv, pc, _p(disp), _p(coords) if coords is not None else None,
+                                                  _p(out), L, radius, B, Cv, D, H, W, W2, _stream(disp)),
+               "geo_lookup")
     del kv, kc
-    _keep_for_replay("lookup", *vol_levels, *corr_levels, disp, out)
+    _keep_for_replay("lookup", *vol_levels, *corr_levels, disp, out, coords)
     return out
 
 
@@ -307,6 +323,7 @@ class PackedConv:
         lo = (ws - hi.float()).half()
         self.whi, self.wlo = hi.contiguous(), lo.contiguous()
         self._sb = {}
+        self._sb_retired = []            # pinned (scale, bias) buffers whose key was reused: kept alive
 
     def scale_bias(self, bias: Tensor = None) -> Tensor:
         """(2^-wexp[co], bias[co]) pairs, 2*Cout floats, for the halo kernels' epilogue, cached per
@@ -324,7 +341,11 @@ class PackedConv:
         key = None if bias is None else (bias.data_ptr(), bias._version)
         hit = self._sb.get(key)
         if hit is not None and hit[1] is not None and hit[1]() is not bias:
-            hit = None                   # the address now belongs to another tensor
+            # the address now belongs to another tensor.  A pinned entry's buffer may still be read by
+            # a captured graph node: it is retired, never dropped, before the key is reused
+            if hit[2]:
+                self._sb_retired.append(hit[0])
+            hit = None
         if hit is None:
             b = torch.zeros_like(self.wscale) if bias is None else bias.detach().float().reshape(-1)
             assert b.numel() == self.cout, f"bias of {b.numel()} for {self.cout} output channels"
@@ -623,7 +644,22 @@ def edgenext_mlp(x: Tensor, res: Tensor, pk1: "PackedConv", bias1: Tensor, pk2: 
     assert res.shape == x.shape, f"edgenext_mlp: res {tuple(res.shape)} vs x {tuple(x.shape)}"
     assert pk1.k == 1 and pk2.k == 1 and pk1.cin == C and pk2.cout == C and pk2.cin == pk1.cout, \
         f"edgenext_mlp: W1 {pk1.cout}x{pk1.cin}, W2 {pk2.cout}x{pk2.cin} for {C} channels"
-    x, res = _c(x), _c(res)
+    if out is not None:
+        # the kernel writes dense NCHW fp32 at out's data pointer: a caller's buffer must be exactly
+        # that, and an in-place update (out is res) must not go through a copy of res
+        _check("edgenext_mlp", out)
+        if tuple(out.shape) != tuple(x.shape) or not out.is_contiguous() or out.device != x.device:
+            raise RuntimeError(f"edgenext_mlp: out must be a contiguous {tuple(x.shape)} fp32 tensor on {x.device}")
+        if out.data_ptr() % 16:
+            raise RuntimeError("edgenext_mlp: out must be 16-byte aligned")
+        if out is res or out.data_ptr() == res.data_ptr():
+            if not res.is_contiguous() or res.data_ptr() % 16:
+                raise RuntimeError("edgenext_mlp: an in-place update (out is res) needs a contiguous, aligned res")
+        elif _overlaps(out, res):
+            raise RuntimeError("edgenext_mlp: out partially overlaps res")
+        if _overlaps(out, x):
+            raise RuntimeError("edgenext_mlp: out must not alias x (x is re-read after out is written)")
+    x, res = _c(x), (res if out is not None and out.data_ptr() == res.data_ptr() else _c(res))
     out = torch.empty_like(x) if out is None else out
     sb1, sb2 = pk1.scale_bias(bias1), pk2.scale_bias(bias2)
     _lib.check(_lib.load().fsmi_edgenext_mlp(_p(x), _p(res), _p(out), _p(pk1.whi), _p(pk1.wlo), _p(sb1), _p(pk2.whi),
@@ -865,15 +901,24 @@ def timer_replay(kernel: str, reps: int = 20) -> float:
     return ms.value
 
 
-def timer_query_clock(kernel: str):
-    """(total_ms, launches) of ``kernel`` since the last reset from the kernel's own clock
-    (first block start to last wave end); lookup and cost-volume build only."""
+def timer_query_clock(kernel: str, captured: bool = False):
+    """(total_ms, launches) of ``kernel`` from the kernel's own clock (first block start to last wave
+    end): the eager launches since the last reset, or (``captured``) the launches baked into graphs
+    captured with ``timer_enable(True, in_capture=True)`` -- their last replay.  Instrumented: lookup,
+    cost-volume build ("comb"), all-pairs correlation ("corr") and its normalisation ("norm"), volume
+    pyramid ("volpyr")."""
     import ctypes
     tot = ctypes.c_double(0.0)
     cnt = ctypes.c_longlong(0)
-    _lib.check(_lib.load().fsmi_timer_query_clock(_lib.KERNELS.index(kernel), ctypes.byref(tot),
-                                                  ctypes.byref(cnt)), "timer_query_clock")
+    fn = _lib.load().fsmi_timer_query_clock_captured if captured else _lib.load().fsmi_timer_query_clock
+    _lib.check(fn(_lib.KERNELS.index(kernel), ctypes.byref(tot), ctypes.byref(cnt)), "timer_query_clock")
     return tot.value, cnt.value
+
+
+def timer_release_captured():
+    """Forget the clock records of captured launches and free their slots; only once every graph
+    captured with ``in_capture=True`` is destroyed (include/fsmi.h)."""
+    _lib.check(_lib.load().fsmi_timer_release_captured(), "timer_release_captured")
 
 
 def timer_query(kernel: str):

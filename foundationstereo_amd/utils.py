@@ -49,13 +49,14 @@ def bilinear_sampler(img, coords, mode="bilinear", mask=False, low_memory=False,
     if check:
         assert bool((coords[..., 1] == 0).all()), "This is a stereo problem"
     P = img.shape[0]
+    dtype = img.dtype                    # the reference returns grid_sample's output in img.dtype
     x = coords[..., 0].reshape(P, -1).float()
     img = img.float()
     if torch_ops.available():
         out = torch_ops.op("bilinear_sampler_1d", img, x)(img, x)
     else:                                # same kernel over the ctypes front end (libfsmi.so alone)
         out = ops.bilinear_sampler_1d(img, x)
-    out = out.reshape(P, img.shape[1], 1, -1)
+    out = out.reshape(P, img.shape[1], 1, -1).to(dtype)
     if mask:
         xg = 2 * x / (W - 1) - 1
         m = ((xg > -1) & (xg < 1)).float().reshape(tuple(coords.shape[:-1]) + (1,))

@@ -94,6 +94,14 @@ int fsmi_geo_lookup(const float* const* vol_levels, const float* const* corr_lev
                     const float* disp, float* out,
                     int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
                     void* stream);
+/* the same with the reference's `coords` argument (core/geometry.py:43,57): coords (B,H,W) fp32, the
+ * column coordinate of each pixel on the left image (core/foundation_stereo.py:231 passes arange(W)
+ * per row), so the corr taps sit at x = coords/2^i - disp/2^i + k.  coords == NULL: the pixel column
+ * w (what fsmi_geo_lookup does, without the load). */
+int fsmi_geo_lookup_coords(const float* const* vol_levels, const float* const* corr_levels,
+                           const float* disp, const float* coords, float* out,
+                           int num_levels, int radius, int B, int Cv, int D, int H, int W, int W2,
+                           void* stream);
 
 /* 1-D stereo specialisation of bilinear_sampler (core/utils/utils.py:44-55):
  * img (P,C,1,Lx); x (P,K) pixel x-coordinates (y == 0); out (P,C,1,K). */
@@ -302,7 +310,7 @@ int fsmi_upsample4_add(const float* t, float* vol, int B, int C, int D, int H, i
 enum {
   FSMI_K_GWC = 0, FSMI_K_CONCAT, FSMI_K_COMB, FSMI_K_PROJ, FSMI_K_CORR, FSMI_K_VOLPYR,
   FSMI_K_LOOKUP, FSMI_K_SAMPLER, FSMI_K_REG, FSMI_K_UPSAMPLE, FSMI_K_GRU_RESET, FSMI_K_GRU_BLEND,
-  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_DWCONV, FSMI_K_RESIZE, FSMI_K_DT, FSMI_K_COUNT
+  FSMI_K_CONV3D, FSMI_K_CONV2D, FSMI_K_DWCONV, FSMI_K_RESIZE, FSMI_K_DT, FSMI_K_NORM, FSMI_K_COUNT
 };
 /* Range guard of the split-precision convs: a block scales its activations by a power of two
  * fixed from its first 32-channel chunk (8 bits of headroom); a later value that would still
@@ -328,11 +336,19 @@ int fsmi_get_range_safe(int* safe);
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
 int fsmi_timer_query(int kernel, double* total_ms, long long* count);
-/* Same launches timed by the kernels themselves (lookup and cost-volume build only): each
+/* Same launches timed by the kernels themselves (lookup, cost-volume build, all-pairs correlation
+ * and its normalisation, volume pyramid): each
  * instrumented launch records its first block start and last wave end (stores acknowledged) in
  * s_memrealtime ticks; returns the summed durations -- execution time without the latency of
  * the event records around the launch. */
 int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count);
+/* The same over the launches captured into hipGraphs while timing was in mode 2: their stamps hold
+ * the last replay of each graph.  Kept across fsmi_timer_reset / fsmi_timer_enable (the graphs keep
+ * writing their slots) until fsmi_timer_release_captured, which the caller may call only once every
+ * graph captured in mode 2 is destroyed (their slots are then handed out again).  Either query fails
+ * (FSMI_ERR_ARG) when a launch of the kernel found the 4M-stamp clock arena full. */
+int fsmi_timer_query_clock_captured(int kernel, double* total_ms, long long* count);
+int fsmi_timer_release_captured(void);
 /* Re-issue the last timed launch of `kernel` (lookup, cost-volume build) `reps` times back to
  * back on its stream between two hipEvents; *avg_ms = span / reps.  The kernels are pure
  * functions of their inputs, so the replays rewrite identical outputs.

@@ -32,9 +32,15 @@ def test_gpus_n_spawns_n_ranks(n):
     assert d["backend"] == "gloo"
     assert d["gathered_ok"] is True
     assert "not a measurement" in d["data"]
+    # a multi-rank line carries parity of pair 0 (rank 0's) and of the last pair (the last rank's,
+    # through the all-gather) -- the model bench builds the same block from the CPU oracle
+    B = 2 * n
+    assert d["parity"]["pairs_checked"] == [0, B - 1]
+    assert d["parity"]["max_abs_dd_px"] == 0.0 and d["parity"]["ok"] is True
 
 
 def test_gpus_1_single_process():
     d, err = _run("--gpus", "1", "--dist-selftest", "--steps", "2", "--warmup", "1")
     assert "launching" not in err
     assert d["n_gpus"] == 1 and d["world_size"] == 1
+    assert d["parity"]["pairs_checked"] == [0]

@@ -558,6 +558,35 @@ def test_edgenext_mlp_vs_fp64(ops_mod, B, H, W, gscale):
     close(yy, out, atol=0, rtol=0)
 
 
+def test_edgenext_mlp_rejects_bad_out(ops_mod):
+    """``out`` is validated, not silently written past: wrong shape, non-contiguous, aliasing x, a
+    partial overlap with res, and an in-place update on a non-contiguous res all raise."""
+    from foundationstereo_amd import update
+    from foundationstereo_amd.submodule import EdgeNextConvEncoder
+    C, B, H, W = 128, 1, 4, 8
+    enc = EdgeNextConvEncoder(C, expan_ratio=4, kernel_size=7, norm=None)
+    synth.init_module_(enc, seed=215)
+    enc = enc.to(DEV).eval()
+    x, y = g(synth.normal(216, (B, C, H, W))), g(synth.normal(217, (B, C, H, W)))
+    with torch.no_grad():
+        pk1, b1 = update._packed(enc.pwconv1)
+        pk2, b2 = update._packed(enc.pwconv2)
+        run = lambda xx, rr, oo: ops_mod.edgenext_mlp(xx, rr, pk1, b1, pk2, b2, gamma=enc.gamma, out=oo)  # noqa: E731
+        with pytest.raises(RuntimeError, match="contiguous"):
+            run(x, y, torch.empty((B, C, H, W + 1), device=DEV))
+        with pytest.raises(RuntimeError, match="contiguous"):
+            run(x, y, torch.empty((B, C, W, H), device=DEV).transpose(2, 3))
+        with pytest.raises(RuntimeError, match="alias x"):
+            run(x, y, x)
+        big = torch.empty((B, C + 1, H, W), device=DEV)
+        big[:, :C] = y
+        with pytest.raises(RuntimeError, match="overlaps res"):
+            run(x, big[:, :C], big[:, 1:])
+        yt = y.transpose(2, 3).contiguous().transpose(2, 3)
+        with pytest.raises(RuntimeError, match="contiguous"):
+            run(x, yt, yt)
+
+
 @pytest.mark.parametrize("shape", [(1, 128, 60, 80), (2, 3, 7, 9), (1, 2, 1, 1), (1, 4, 30, 40)])
 def test_pool2x_vs_torch(ops_mod, shape):
     """pool2x (avg 3x3, stride 2, pad 1, count_include_pad) vs the torch CPU fp32 op."""
@@ -678,6 +707,46 @@ def test_lookup_batched_ragged(ops_mod, B, H, W, D, L):
     ref = oracle.GeoEncoding(t(f1), t(f2), t(vol), L, 4)
     coords = torch.arange(W, dtype=torch.float).view(1, 1, W, 1).repeat(B, H, 1, 1)
     close(out, ref(t(disp), coords), atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["arange", "shifted", "random"])
+def test_lookup_coords_vs_oracle(ops_mod, kind):
+    """The reference's ``coords`` argument (core/geometry.py:43,57) honoured, not assumed: the
+    arange(W) the reference passes (same result as coords=None), a shifted / fractional grid and
+    arbitrary per-pixel columns (beyond the image too), each against the oracle's restatement of
+    ``__call__`` with the same coords; also through torch.ops.fsmi.geo_lookup."""
+    from foundationstereo_amd import torch_ops
+    from foundationstereo_amd.geometry import Combined_Geo_Encoding_Volume
+    B, C, Cv, H, W, D, L = 2, 32, 28, 3, 40, 32, 4
+    f1, f2 = synth.normal(71, (B, C, H, W)), synth.normal(72, (B, C, H, W))
+    vol = synth.normal(73, (B, Cv, D, H, W))
+    disp = synth.uniform(74, (B, 1, H, W), -4.0, D + 4.0)
+    coords = torch.arange(W, dtype=torch.float).view(1, 1, W, 1).repeat(B, H, 1, 1)
+    if kind == "shifted":
+        coords = coords + 2.75
+    elif kind == "random":
+        coords = t(synth.uniform(75, (B, H, W, 1), -6.0, W + 6.0))
+    ge = Combined_Geo_Encoding_Volume(g(f1), g(f2), g(vol), num_levels=L, dx=torch.linspace(-4, 4, 9))
+    out = ge(g(disp), g(coords))
+    ref = oracle.GeoEncoding(t(f1), t(f2), t(vol), L, 4)(t(disp), coords)
+    close(out, ref, atol=1e-5)
+    if kind == "arange":
+        assert torch.equal(out, ge(g(disp)))
+    else:
+        assert float((out - ge(g(disp))).abs().max()) > 1e-3     # coords really moved the corr taps
+    if torch_ops.available():
+        op = torch.ops.fsmi.geo_lookup(ge.geo_volume_pyramid, ge.init_corr_pyramid, g(disp), 4, g(coords))
+        assert torch.equal(op, out)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_bilinear_sampler_returns_img_dtype(ops_mod, gold, dtype):
+    """core/utils/utils.py:50-51: the grid is cast to img.dtype and grid_sample returns img.dtype."""
+    from foundationstereo_amd.utils import bilinear_sampler
+    img = g(gold["bs_img"]).to(dtype)
+    out = bilinear_sampler(img, g(gold["bs_coords"]))
+    assert out.dtype == dtype
+    close(out.float(), gold["bs_out"], atol=1e-5 if dtype == torch.float32 else 2e-2)
 
 
 def test_bilinear_sampler_golden(ops_mod, gold):
