@@ -46,6 +46,7 @@ SIGNATURES = {
     "fsmi_conv3d_halo_x3_ex": [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                                _P, ctypes.c_longlong, _P],
     "fsmi_conv3d_up2_halo_x3": [_P, _I, _PP, _PP, _PP, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_conv2d_up2_halo_x3": [_P, _I, _PP, _PP, _PP, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_edgenext_mlp": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],

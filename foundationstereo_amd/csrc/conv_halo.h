@@ -110,12 +110,14 @@ struct HaloArgs {
   int gHd;
   int* ovf;                        // range flag (host-mapped; set to 1 when a scaled value overflows fp16)
   int pipe;                        // 2D register-weight tiles: the pipelined-staging variant (cfg 32 + c)
-  // transposed-conv phase launches (fsmi_conv3d_up2_halo_x3; all 0 otherwise): the input window
-  // shifted by (sd, sh, sw) in {0, 1}, and output voxel (d, h, w) written at (2d + od, 2h + oh,
-  // 2w + ow) of the (2D, 2H, 2W) output, whose channel stride is ocstride
+  // transposed-conv phase launches (fsmi_conv3d_up2_halo_x3 / fsmi_conv2d_up2_halo_x3; all 0
+  // otherwise): the input window shifted by (sd, sh, sw) in {0, 1}, and output voxel (d, h, w)
+  // written at (2d + od, 2h + oh, 2w + ow) of the (2D, 2H, 2W) output (2D maps: od = 0, D = 1),
+  // whose channel stride is ocstride
   int up, sd, sh, sw, od, oh, ow;
   long long ocstride;
-  // up == 2: all eight phases in one launch (blocks phase-major), phase p's weights / scale-bias
+  // up == 2: all eight phases of a volume in one launch (blocks phase-major); up == 4: the four
+  // phases of a 2D map.  Phase p's weights / scale-bias
   const _Float16* whi8[8];
   const _Float16* wlo8[8];
   const float2* sb8[8];
@@ -317,7 +319,7 @@ __device__ __forceinline__ void store_frag_c(const HaloArgs& a, const f32x16& v,
   // emitted s_waitcnt vmcnt(0) after every store, ~128 serialised store round trips per wave
   // (20 us of a 185 us block, round 3).  Rows past Cout only exist in the last cout tile.
   const long long HW = a.cstride;
-  const long long OHW = RESPRE && a.up ? a.ocstride : HW;   // output channel stride (transposed conv)
+  const long long OHW = a.up ? a.ocstride : HW;   // output channel stride (transposed conv)
   const bool full = (cb - (cb & 4)) + 32 <= a.Cout;          // all 32 rows of the fragment exist
   if constexpr (ACT >= 3 && ACT <= 5) {
     float ghv[16], gzv[16], ov[16];
@@ -759,8 +761,9 @@ __device__ __forceinline__ void frag_coef_lds(float xinv, int cl, const float2* 
   }
 }
 
-// Non-split epilogue of the block's tile with the activation fixed at compile time
-template <int ACT, int TM, int TN, bool D3>
+// Non-split epilogue of the block's tile with the activation fixed at compile time.  UP: the
+// instantiation may run transposed-conv phases (volumes, and the 2x2 kernel on 2D maps)
+template <int ACT, int TM, int TN, bool D3, bool UP = D3>
 __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv, const TileCoord& t,
                                          int wm, int wn, int lane, unsigned fown, const float2* lsb, const float* lg) {
   const int hsel = lane >> 5, rl = lane & 31;
@@ -768,9 +771,11 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
   for (int j = 0; j < TN; ++j) {
     const int hh = t.r0 + wn * TN + j, ww = t.c0 + rl;
     if (hh >= a.H || ww >= a.W) continue;
-    const long long hw = D3 && a.up ? (static_cast<long long>(2 * t.d0 + a.od) * 2 * a.H + 2 * hh + a.oh) * 2 * a.W
-                                          + 2 * ww + a.ow
-                                    : static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
+    // transposed-conv phases (KS == 2 on 2D maps, or any volume launch with up set): the output
+    // pixel of input (d0, hh, ww) in phase (od, oh, ow); 2D maps have d0 = od = 0
+    const long long hw = UP && a.up
+                             ? (static_cast<long long>(2 * t.d0 + a.od) * 2 * a.H + 2 * hh + a.oh) * 2 * a.W + 2 * ww + a.ow
+                             : static_cast<long long>(t.d0) * a.H * a.W + hh * a.W + ww;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
       if ((fown >> (i * TN + j)) & 1u) {
@@ -784,7 +789,7 @@ __device__ __forceinline__ void epi_tile(const HaloArgs& a, const f32x16 (&acc)[
 }
 
 // n = lane&31 is the pixel column, tile row wn*TN + j; D row map of the 32x32 MFMA
-template <int TM, int TN, bool D3>
+template <int TM, int TN, bool D3, bool UP = D3>
 __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&acc)[TM][TN], float xinv,
                                               const TileCoord& t, int wm, int wn, int lane, bool partial,
                                               const float2* lsb, const float* lg, unsigned fown = ~0u) {
@@ -810,13 +815,13 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
     return;
   }
   switch (a.act) {                 // uniform: one specialised tile epilogue per activation
-    case 1: epi_tile<1, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
-    case 2: epi_tile<2, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
-    case 3: epi_tile<3, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
-    case 4: epi_tile<4, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
-    case 5: epi_tile<5, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
-    case 6: epi_tile<6, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
-    default: epi_tile<0, TM, TN, D3>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 1: epi_tile<1, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 2: epi_tile<2, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 3: epi_tile<3, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 4: epi_tile<4, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 5: epi_tile<5, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 6: epi_tile<6, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    default: epi_tile<0, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
   }
 }
 
@@ -986,7 +991,8 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
     }
   }
   flag_overflow(a, ovf);
-  conv_epilogue<TM, TN, D3>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1, ecoef.sb, ecoef.g);
+  conv_epilogue<TM, TN, D3, D3 || KS == 2>(a, acc, exp2i(sx == kNoExp ? 0 : -sx), tc, wm, wn, lane, a.nsplit > 1,
+                                           ecoef.sb, ecoef.g);
 }
 
 // ---------------------------------------------------------------- cfg 2/3: weights in registers
@@ -1206,7 +1212,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
       }
       xinv = 1.f;
     }
-    conv_epilogue<TM, TN, D3>(a, acc, xinv, tc, wm, wn, lane, partial, ecoef.sb, ecoef.g, fown);
+    conv_epilogue<TM, TN, D3, D3 || KS == 2>(a, acc, xinv, tc, wm, wn, lane, partial, ecoef.sb, ecoef.g, fown);
     if (tsb && threadIdx.x == 0) {
       tsb[38] = wall_clock64();
       tsb[39] = (static_cast<unsigned long long>(cc_end - cc_begin) << 32) | blockIdx.x;
@@ -1215,8 +1221,8 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
 
   unsigned bid = blockIdx.x, nb = gridDim.x;
   if constexpr (KS == 2) {
-    if (a.up == 2) {                               // transposed-conv phases, phase-major blocks
-      nb /= 8;
+    if (a.up == 2 || a.up == 4) {                  // transposed-conv phases, phase-major blocks
+      nb = a.up == 2 ? nb / 8 : nb / 4;
       const int ph = static_cast<int>(bid / nb);
       bid -= static_cast<unsigned>(ph) * nb;
       // constant indices only (a dynamic index into the by-value args puts them in scratch)
@@ -1228,8 +1234,13 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
           a.sb = a.sb8[q];
         }
       }
-      a.sd = a.od = ph >> 2;
-      a.sh = a.oh = (ph >> 1) & 1;
+      if (a.up == 2) {
+        a.sd = a.od = ph >> 2;
+        a.sh = a.oh = (ph >> 1) & 1;
+      } else {                                     // 2D map: phase = (oh, ow)
+        a.sd = a.od = 0;
+        a.sh = a.oh = ph >> 1;
+      }
       a.sw = a.ow = ph & 1;
     }
   }
@@ -1384,7 +1395,7 @@ __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
 
 template <int KS, int BM, int TR, int WM, bool WREG, bool D3, int KG = 1, int STR = 1>
 void launch_tile(const HaloArgs& a, hipStream_t s) {
-  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit * (a.up == 2 ? 8 : 1);
+  const unsigned grid = static_cast<unsigned>(a.npix) * a.nco * a.nsplit * (a.up == 2 ? 8 : a.up == 4 ? 4 : 1);
   if constexpr (WREG && !D3 && KG == 1 && STR == 1 && KS != 2) {
     if (a.pipe) {                                  // cfg 32 + c: the pipelined-staging variant
       hipLaunchKernelGGL((conv_halo_pipe_kernel<KS, BM, TR, WM>), dim3(grid), dim3(256), 0, s, a);

@@ -111,7 +111,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(scale_bias) % 8 == 0, "%s: scale_bias must be 8-B aligned", what);
   FSMI_CHECK_ARG(nseg >= 1 && nseg <= kHMaxSeg, "%s: 1..%d segments, got %d", what, kHMaxSeg, nseg);
   FSMI_CHECK_ARG(B > 0 && Cout > 0 && H > 0 && W > 0, "%s: bad shape", what);
-  FSMI_CHECK_ARG(KS == 1 || KS == 3 || (KS == 2 && a.up && KD == 2), "%s: kernel %d unsupported (1, 3)", what, KS);
+  FSMI_CHECK_ARG(KS == 1 || KS == 3 || (KS == 2 && ((a.up == 2 && KD == 2) || (a.up == 4 && KD == 1 && D == 1))),
+                 "%s: kernel %d unsupported (1, 3; 2 only for transposed-conv phases)", what, KS);
   if (a.str == 0) a.str = 1;
   FSMI_CHECK_ARG(a.str == 1 || (a.str == 2 && (KS == 3 || KS == 1) && (KD == 3 || KD == 1) && !a.up),
                  "%s: stride 2 needs a KD x KS x KS kernel with KS, KD in {1, 3}", what);
@@ -257,7 +258,7 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   }();
   a.dbg = conv_dbg;
   g_cfg_launches[(a.pipe ? 32 : 0) + (kg == 2 ? 16 : 0) + cfg].fetch_add(1, std::memory_order_relaxed);
-  const int rc = a.str == 2 ? halo::launch_s2(KS, cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
+  const int rc = a.str == 2 ? halo::launch_s2(KS, cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? (d3 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : halo::launch_cfg<2, false>(cfg, kg, a, s)) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;
   if (a.nsplit > 1) halo::split_reduce(a, s);
@@ -403,4 +404,38 @@ extern "C" int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* cons
                           8 * Cout, 0, B, Cout, 2, H, W, cfg, 1, nullptr, 0, stream, D, 2);
   if (rc != FSMI_OK) return rc;
   return FSMI_OK;
+}
+
+extern "C" int fsmi_conv2d_up2_halo_x3(const float* x, int Cin, const void* const* whi, const void* const* wlo,
+                                       const float* const* scale_bias, float* out, int B, int Cout, int H, int W,
+                                       int act, int cfg, void* stream) {
+  FSMI_CHECK_ARG(x && out && whi && wlo && scale_bias && Cin > 0, "fsmi_conv2d_up2_halo_x3: null pointer / channels");
+  FSMI_CHECK_ARG(act == 0 || act == 1 || act == 6, "fsmi_conv2d_up2_halo_x3: act %d (0, 1, 6)", act);
+  // ConvTranspose2d(k=4, s=2, p=1) as four 2x2 stride-1 phase convs over the input (the 2D analogue of
+  // fsmi_conv3d_up2_halo_x3); 32-cout x 4-row tiles unless told otherwise (the spx layers: 32 and 9 couts)
+  if (cfg < 0) cfg = Cout > 64 ? 3 : (Cout > 32 ? 5 : 7);
+  FSMI_CHECK_ARG(cfg == 2 || cfg == 3 || cfg == 5 || cfg == 6 || cfg == 7,
+                 "fsmi_conv2d_up2_halo_x3: tile %d (2, 3, 5, 6, 7)", cfg);
+  HaloArgs a{};
+  for (int p = 0; p < 4; ++p) {
+    FSMI_CHECK_ARG(whi[p] && wlo[p] && scale_bias[p], "fsmi_conv2d_up2_halo_x3: null phase %d", p);
+    FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(scale_bias[p]) % 8 == 0, "fsmi_conv2d_up2_halo_x3: scale_bias align");
+    a.whi8[p] = static_cast<const _Float16*>(whi[p]);
+    a.wlo8[p] = static_cast<const _Float16*>(wlo[p]);
+    a.sb8[p] = reinterpret_cast<const float2*>(scale_bias[p]);
+  }
+  for (int p = 4; p < 8; ++p) {       // never selected (four phases); keep the array defined
+    a.whi8[p] = a.whi8[0];
+    a.wlo8[p] = a.wlo8[0];
+    a.sb8[p] = a.sb8[0];
+  }
+  a.act = act;
+  a.alpha = 1.f;
+  a.up = 4;                                       // the four phases of a 2D map in one launch
+  a.ocstride = 4ll * H * W;
+  const float* seg[1] = {x};
+  const int ch[1] = {Cin}, tot[1] = {Cin};
+  // out_ctot = 4 * Cout: run_halo's batch stride (out_ctot x the input plane) is the (Cout, 2H, 2W) output's
+  return run_halo(a, "fsmi_conv2d_up2_halo_x3", seg, ch, tot, 1, whi[0], wlo[0], scale_bias[0], out, 4 * Cout, 0, B,
+                  Cout, 2, H, W, cfg, 1, nullptr, 0, stream, 1, 1);
 }

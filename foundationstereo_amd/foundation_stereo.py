@@ -296,7 +296,11 @@ class FoundationStereo(nn.Module):
         """core/foundation_stereo.py:183-191: returns (B,1,H,W) fp32."""
         with autocast(self.args.mixed_precision, self.args.get("mixed_dtype", "float16")):
             xspx = self.spx_2_gru(mask_feat_4, stem_2x)
-            logits = self.spx_gru(xspx)
+            spx = self.spx_gru[0]
+            if len(self.spx_gru) == 1 and _sub.fast_up2d(xspx, spx):
+                logits = _sub.deconv2d_bn_act(xspx, spx)      # ConvTranspose2d(64, 9, 4, 2, 1) + bias on HIP
+            else:
+                logits = self.spx_gru(xspx)
         return ops.softmax_context_upsample(disp.float(), logits.float(), 4.0).unsqueeze(1)
 
     def forward(self, image1, image2, iters=12, flow_init=None, test_mode=False, low_memory=False, init_disp=None):

@@ -466,6 +466,45 @@ def conv3d_up2(x: Tensor, packs, bias: Tensor = None, act=None, cfg: int = -1) -
     return out
 
 
+def pack_deconv2d_phases(weight: Tensor, scale: Tensor = None):
+    """ConvTranspose2d(k=4, s=2, p=1) weight (Cin, Cout, 4, 4), optionally scaled per output channel
+    (folded BatchNorm), as the 4 phase convs (2x2, stride 1) of ``fsmi_conv2d_up2_halo_x3``."""
+    w = weight.detach().double()
+    assert w.dim() == 4 and tuple(w.shape[2:]) == (4, 4), "pack_deconv2d_phases: k = 4 only"
+    if scale is not None:
+        w = w * scale.detach().double().view(1, -1, 1, 1)
+    packs = []
+    for p in range(4):
+        ph, pw = p >> 1, p & 1
+        kh = [_UP2_K[ph][t] for t in range(2)]
+        kw = [_UP2_K[pw][t] for t in range(2)]
+        wp = w[:, :, kh][:, :, :, kw]                            # (Cin, Cout, 2, 2)
+        packs.append(PackedConv(wp.permute(1, 0, 2, 3).float().contiguous(), mode="halo"))
+    return packs
+
+
+def conv2d_up2(x: Tensor, packs, bias: Tensor = None, act=None, cfg: int = -1) -> Tensor:
+    """ConvTranspose2d(k=4, s=2, p=1) (+ bias / folded BN, activation) on the halo kernel's 2x2 phase
+    tiles: (B, Cin, H, W) -> (B, Cout, 2H, 2W)."""
+    assert len(packs) == 4 and all(pk.mode == "halo" and pk.k == 2 and pk.kd == 1 for pk in packs)
+    _check("conv2d_up2", x, *([bias] if bias is not None else []))
+    B, Cin, H, W = x.shape
+    pk0 = packs[0]
+    assert Cin == pk0.cin, f"conv2d_up2: {Cin} input channels for a conv packed with {pk0.cin}"
+    x = _c(x)
+    out = torch.empty((B, pk0.cout, 2 * H, 2 * W), device=x.device, dtype=torch.float32)
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * Cin * pk0.cout * 16 * B * H * W
+    whi, k1 = _lib.ptr_array([_p(pk.whi) for pk in packs])
+    wlo, k2 = _lib.ptr_array([_p(pk.wlo) for pk in packs])
+    sbs = [pk.scale_bias(bias) for pk in packs]
+    sb, k3 = _lib.ptr_array([_p(t) for t in sbs])
+    _lib.check(_lib.load().fsmi_conv2d_up2_halo_x3(_p(x), Cin, whi, wlo, sb, _p(out), B, pk0.cout, H, W,
+                                                   _ACT3D[act], cfg, _stream(x)), "conv2d_up2")
+    del k1, k2, k3
+    return out
+
+
 _GATE_MODE = {"zr": 0, "blend_small": 1, "blend_large": 2}
 
 _RANGE_DEBUG = os.environ.get("FSMI_RANGE_DEBUG", "0") == "1"   # diagnostics: sync + check after each conv

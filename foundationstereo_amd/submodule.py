@@ -60,6 +60,9 @@ FILTER3D = os.environ.get("FSMI_FILTER3D", "1") != "0"
 UP3D = os.environ.get("FSMI_UP3D", "1") != "0"
 UP3D_MINVOX = int(os.environ.get("FSMI_UP3D_MINVOX", "0"))
 DT_FAST = os.environ.get("FSMI_DT", "1") != "0"
+# the spx ConvTranspose2d(k=4, s=2, p=1) pair (spx_2_gru.conv1, spx_gru) on the halo kernel's 2x2 phase
+# tiles (FSMI_UP2D=0: MIOpen, for A/B)
+UP2D = os.environ.get("FSMI_UP2D", "1") != "0"
 # stride-2 3x3x3 convs on the halo kernel's stride-2 tiles (FSMI_S2=0: MIOpen, for A/B)
 S2_3D = os.environ.get("FSMI_S2", "1") != "0"
 # FeatureAtt's sigmoid(gate) * cv folded into the producing conv's epilogue (FSMI_FATT=0: ATen)
@@ -157,10 +160,28 @@ def _fast_up3d(x, conv, bn) -> bool:
                                                          and bn.track_running_stats)
 
 
+def fast_up2d(x, conv, bn=None) -> bool:
+    """ConvTranspose2d(k=4, s=2, p=1) (+ eval BatchNorm2d) that the 2x2 phase tiles run."""
+    if not (UP2D and x.is_cuda and x.dtype in HIP_DTYPES and not torch.is_grad_enabled()
+            and type(conv) is nn.ConvTranspose2d):
+        return False
+    if conv.kernel_size != (4, 4) or conv.stride != (2, 2) or conv.padding != (1, 1) \
+            or conv.output_padding != (0, 0) or conv.dilation != (1, 1) or conv.groups != 1:
+        return False
+    return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm2d and not bn.training
+                                                         and bn.track_running_stats)
+
+
+def deconv2d_bn_act(x, conv, bn=None, act=None):
+    """act(bn(conv_transpose2d(x))) on the 2x2 phase tiles (see ``fast_up2d``)."""
+    packs, b = _packed_up(conv, bn)
+    return ops.conv2d_up2(_f32(x), packs, bias=b, act=act)
+
+
 def _packed_up(conv, bn):
-    """The 8 phase packs of a ConvTranspose3d with its eval BatchNorm folded (fp64 fold), cached."""
+    """The 8 (4) phase packs of a ConvTranspose3d (2d) with its eval BatchNorm folded (fp64 fold), cached."""
     ts = [conv.weight] + ([conv.bias] if conv.bias is not None else [])
-    is_bn = isinstance(bn, nn.BatchNorm3d)
+    is_bn = isinstance(bn, (nn.BatchNorm2d, nn.BatchNorm3d))
     if is_bn:
         ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
     key = tuple((t.data_ptr(), t._version) for t in ts)
@@ -174,7 +195,8 @@ def _packed_up(conv, bn):
             if is_bn:
                 sc = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
                 b = (b - bn.running_mean.double()) * sc + bn.bias.double()
-            hit = (key, ops.pack_deconv_phases(conv.weight, sc), b.float().contiguous())
+            pack = ops.pack_deconv2d_phases if conv.weight.dim() == 4 else ops.pack_deconv_phases
+            hit = (key, pack(conv.weight, sc), b.float().contiguous())
         conv.__dict__["_fsmi_pack_up"] = hit
     return hit[1], hit[2]
 
@@ -260,6 +282,8 @@ class BasicConv(nn.Module):
             return ops.conv3d_up2(_f32(x), packs, bias=b, act="leaky" if self.relu else None)
         if _fast2d(x, self.conv, bn):
             return conv2d_bn_act([x], self.conv, bn, "leaky" if self.relu else None)
+        if fast_up2d(x, self.conv, bn):             # ConvTranspose2d k4 s2: 4 phase convs, BN folded
+            return deconv2d_bn_act(x, self.conv, bn, "leaky" if self.relu else None)
         x = self.bn(self.conv(x)) if self.use_bn else self.conv(x)
         return F.leaky_relu(x, 0.01) if self.relu else x
 
@@ -445,6 +469,11 @@ class Conv2x(nn.Module):
         x = self.conv1(x)
         if x.shape != rem.shape:
             x = F.interpolate(x, size=(rem.shape[-2], rem.shape[-1]), mode="bilinear")
+        c2 = self.conv2
+        bn2 = c2.bn if c2.use_bn else None
+        if self.concat and not self.is_3d and x.shape[1] % 8 == 0 and _fast2d(x, c2.conv, bn2):
+            # the cat read in place: conv2's input is the two segments (x, rem)
+            return conv2d_bn_act([x, rem], c2.conv, bn2, "leaky" if c2.relu else None)
         x = torch.cat((x, rem), 1) if self.concat else x + rem
         return self.conv2(x)
 

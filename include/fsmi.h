@@ -258,6 +258,13 @@ int fsmi_conv3d_halo_x3_ex(const float* x, int Cin, const void* whi, const void*
 int fsmi_conv3d_up2_halo_x3(const float* x, int Cin, const void* const* whi, const void* const* wlo,
                             const float* const* scale_bias, float* out, int B, int Cout, int D, int H, int W,
                             int act, int cfg, void* stream);
+/* ConvTranspose2d(k=4, s=2, p=1) (+ bias / folded BN, activation 0 / 1 ReLU / 6 LeakyReLU) on 2x2
+ * phase tiles: x (B,Cin,H,W) -> out (B,Cout,2H,2W); whi / wlo / scale_bias: the 4 phase packs
+ * (phase p = 2*oh + ow writes output pixels (2h + oh, 2w + ow)).  Replaces the spx upsampling
+ * deconvs spx_2_gru.conv1 and spx_gru (core/foundation_stereo.py:183-191, core/submodule.py:281-317). */
+int fsmi_conv2d_up2_halo_x3(const float* x, int Cin, const void* const* whi, const void* const* wlo,
+                            const float* const* scale_bias, float* out, int B, int Cout, int H, int W,
+                            int act, int cfg, void* stream);
 
 int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
                   int H, int W, void* stream);

@@ -244,6 +244,58 @@ def test_conv3d_up2_vs_torch(ops_mod, cin, cout, D, H, W, B, cfg):
     close(out, ref, atol=2e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("cfg", [-1, 2, 3, 5, 6, 7])
+@pytest.mark.parametrize("cin,cout,H,W,B,act", [(32, 32, 60, 80, 1, "leaky"), (64, 9, 24, 37, 2, None),
+                                                (40, 70, 9, 33, 1, "relu"), (64, 130, 5, 65, 1, None)])
+def test_conv2d_up2_vs_torch(ops_mod, cin, cout, H, W, B, act, cfg):
+    """ConvTranspose2d(k=4, s=2, p=1) (+ bias / folded scale, activation) as 4 phase convs on the 2x2
+    halo tiles vs fp64 torch: the spx pair's shapes (32 -> 32 + LeakyReLU, 64 -> 9 + bias;
+    core/foundation_stereo.py:183-191), ragged rows / columns / couts / channel chunks, batch 2."""
+    import torch.nn.functional as F
+    gen = torch.Generator().manual_seed(cin * 7 + cout + H)
+    x = torch.randn(B, cin, H, W, generator=gen)
+    w = torch.randn(cin, cout, 4, 4, generator=gen) * 0.05
+    sc = torch.rand(cout, generator=gen) + 0.5
+    sh = torch.randn(cout, generator=gen) * 0.1
+    packs = ops_mod.pack_deconv2d_phases(g(w), g(sc))
+    out = ops_mod.conv2d_up2(g(x), packs, bias=g(sh), act=act, cfg=cfg)
+    ref = F.conv_transpose2d(x.double(), w.double(), stride=2, padding=1) * sc.double().view(1, -1, 1, 1) \
+        + sh.double().view(1, -1, 1, 1)
+    ref = {"leaky": lambda v: F.leaky_relu(v, 0.01), "relu": F.relu, None: lambda v: v}[act](ref)
+    assert out.shape == ref.shape
+    close(out, ref, atol=2e-5, rtol=1e-5)
+
+
+def test_spx_deconvs_on_hip(ops_mod, monkeypatch):
+    """upsample_disp's ConvTranspose2d pair (spx_2_gru.conv1, spx_gru) runs on the phase tiles, never
+    through torch (MIOpen), and equals the torch modules (fp64) on the same input."""
+    import torch.nn.functional as F
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    args = synth.make_args(max_disp=32, corr_levels=2, vit_size="vits")
+    m = FoundationStereo(args).eval()
+    synth.init_module_(m, seed=77)
+    m = m.to(DEV)
+    B, H4, W4 = 1, 16, 24
+    disp = g(synth.uniform(78, (B, 1, H4, W4), 0.0, 8.0))
+    mask = g(synth.normal(79, (B, 32, H4, W4)))
+    stem = g(synth.normal(80, (B, 32, 2 * H4, 2 * W4)))
+    m64 = m.double()
+    with torch.no_grad():
+        x1 = F.leaky_relu(m64.spx_2_gru.conv1.conv(mask.double()), 0.01)
+        x2 = m64.spx_2_gru.conv2(torch.cat((x1, stem.double()), 1))
+        lg = m64.spx_gru(x2)
+        ref = oracle.context_upsample(disp.double().cpu() * 4.0, torch.softmax(lg.cpu(), 1))
+    m = m.float()
+
+    def refuse(*a, **k):
+        raise AssertionError("conv_transpose2d reached torch")
+    monkeypatch.setattr(F, "conv_transpose2d", refuse)
+    monkeypatch.setattr(torch, "conv_transpose2d", refuse)
+    with torch.no_grad():
+        out = m.upsample_disp(disp, mask, stem)
+    close(out.squeeze(1), ref, atol=2e-4, rtol=1e-5)
+
+
 @pytest.mark.parametrize("cfg,nsplit", [(-1, -1), (4, 1), (5, 1), (7, 1), (10, 1), (10, 3), (4, 2)])
 @pytest.mark.parametrize("cin,cout,D,H,W,B", [(28, 56, 12, 19, 70, 1), (56, 112, 7, 10, 40, 2),
                                               (112, 168, 6, 15, 20, 1), (40, 37, 5, 9, 65, 1)])

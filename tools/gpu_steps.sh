@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU steps, one parametrised script (replaces the per-call tools/rounds/*.sh).
-#   bash tools/gpu_r4.sh STEP [STEP ...]      (each STEP's output under gpurun_out/r4/<STEP>)
+# GPU steps, one parametrised script (output under $GPU_OUT, default gpurun_out/r5).
+#   bash tools/gpu_steps.sh STEP [STEP ...]
 # Steps:
 #   test        pytest -m gpu (per-test timeout, stops at the first failure)
 #   bench       bench.py cfg2 (20 steps) -> bench_cfg2.json
@@ -16,7 +16,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r4
+OUT=${GPU_OUT:-gpurun_out/r5}
 mkdir -p $OUT
 BENCH_ARGS=${BENCH_ARGS:-}
 fail() { echo "$1 rc=$2"; tail -20 "$3"; exit 1; }
