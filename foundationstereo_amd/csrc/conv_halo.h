@@ -465,6 +465,11 @@ __device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], i
 // multiple.  Computed once per staging call from kernel arguments (scalar registers); per lane
 // only the segment select and one multiply-add remain (the per-lane select of pointer, batch
 // stride and first channel plus two 64-bit products was ~60 VALU per 8-channel task).
+// chan() returns a GLOBAL (address space 1) pointer: a pointer rebuilt from an integer is generic,
+// and loads through it were flat_load_dword -- which count in lgkmcnt as well as vmcnt, so every
+// LDS operand wait after a chunk's halo loads also waited for those HBM loads (round 5).
+typedef const __attribute__((address_space(1))) float* gcfptr;
+
 struct SegBases {
   uintptr_t p[kHMaxSeg];
   __device__ __forceinline__ void init(const HaloArgs& a, int b, long long HW) {
@@ -476,11 +481,11 @@ struct SegBases {
       start = a.seg_end[q];
     }
   }
-  __device__ __forceinline__ const float* chan(const HaloArgs& a, int ci, long long HW) const {
+  __device__ __forceinline__ gcfptr chan(const HaloArgs& a, int ci, long long HW) const {
     uintptr_t sp = p[0];
 #pragma unroll
     for (int q = 1; q < kHMaxSeg; ++q) sp = (q < a.nseg && ci >= a.seg_end[q - 1]) ? p[q] : sp;
-    return reinterpret_cast<const float*>(sp) + static_cast<long long>(ci) * HW;
+    return reinterpret_cast<gcfptr>(sp) + static_cast<long long>(ci) * HW;
   }
 };
 
@@ -527,7 +532,7 @@ struct HaloStage {
       const int cic = min(ci0, a.Cin - 1);
       // segment of this 8-channel group (segments hold multiples of 8 channels): a select chain
       // over constant indices, so the kernarg arrays are never indexed per lane
-      const float* src = seg.chan(a, cic, HW) + poff + pix;
+      const gcfptr src = seg.chan(a, cic, HW) + poff + pix;
       const bool ok = (desc[u] & 4) && plane_ok;
       f32x8 v;
       if (full) {

@@ -47,7 +47,7 @@ __device__ __forceinline__ void wait_lgkm0() {     // lgkmcnt = 0, vmcnt / expcn
 // the M0 write -> LDS-DMA hazard needs one wait state (s_nop 0) inside the string.  Without both,
 // a DMA could use a stale M0 (another ring slot) or leave the compiler's M0 clobbered: rare wrong
 // partial sums in the split-K pointwise tests (round 4: 1 of ~40 runs; fixed here).
-__device__ __forceinline__ void dma16(const float* src, float* dst) {
+__device__ __forceinline__ void dma16(gcfptr src, float* dst) {
   typedef __attribute__((address_space(3))) float lds_float;
   const unsigned lds = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(reinterpret_cast<size_t>((lds_float*)dst)));
   unsigned keep;

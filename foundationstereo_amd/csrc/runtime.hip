@@ -127,7 +127,9 @@ int range_safe() { return __atomic_load_n(&g_range_safe, __ATOMIC_RELAXED); }
 // forward, so a replay that overflowed never returns a finite disparity (fsmi_range_poison)
 __global__ __launch_bounds__(256) void range_poison_kernel(const int* flag, float* out, long long n) {
   __shared__ int f;
-  if (threadIdx.x == 0) f = *reinterpret_cast<const volatile int*>(flag);
+  // a system-scope atomic load of the host-mapped flag (global_load ... sc0 sc1; a volatile load
+  // became a flat load)
+  if (threadIdx.x == 0) f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __syncthreads();
   if (!f) return;
   for (long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x; i < n;

@@ -56,3 +56,23 @@ def test_wrong_weight_load_count_is_flagged(tmp_path):
     assert len(res) == PW_TILES
     for name, r in res.items():
         assert any(w["unsafe"] for w in r["waits"]), (cdw.short(name), r["waits"])
+
+
+@pytest.mark.parametrize("lib", LIBS, ids=os.path.basename)
+def test_no_flat_memory_ops(lib):
+    """No kernel accesses memory through FLAT instructions.  A flat load counts in lgkmcnt as well as
+    vmcnt, so the LDS-operand waits of the conv main loops also waited for the halo loads in flight
+    (HBM latency inside the MFMA stream): round 4's halo staging built its pointers from integers
+    (conv_halo.h SegBases) and every halo conv kernel staged through flat_load_dword."""
+    if not os.path.exists(lib):
+        pytest.skip(f"{os.path.basename(lib)} not built (__graft_entry__.build())")
+    bad = {}
+    for co in cdw.code_objects(lib):
+        cur = None
+        for line in cdw.disassemble(co).splitlines():
+            m = cdw._SYM.match(line)
+            if m:
+                cur = m.group(2)
+            elif "\tflat_" in line:
+                bad[cur] = bad.get(cur, 0) + 1
+    assert not bad, {k[:90]: v for k, v in list(bad.items())[:10]}
