@@ -69,6 +69,7 @@ SIGNATURES = {
     "fsmi_timer_replay": [_I, _I, ctypes.POINTER(ctypes.c_double)],
     "fsmi_timer_query_clock_captured": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
     "fsmi_timer_release_captured": [],
+    "fsmi_timer_dump_captured": [ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",

@@ -38,6 +38,7 @@ __device__ __forceinline__ int wslot(int row, int s) { return s ^ ((row >> 2) & 
 
 template <int KD>
 __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
+
   constexpr int DB = kDepthDB, TR = kDepthTR, JW = DB / 2, PD = KD / 2;
   static_assert(JW == 8, "the A-fragment ring holds 8 taps: 8 outputs per wave");
   using HS = HaloStage<1, TR>;
@@ -227,6 +228,9 @@ int launch_depth(HaloArgs& a, hipStream_t s) {
   a.nct = (a.W + 31) / 32;
   const long long ndt = (a.D + kDepthDB - 1) / kDepthDB;
   const long long grid = static_cast<long long>(a.CoutP / 32) * a.B * a.nrt * a.nct * ndt;
+  // no in-kernel clock: the tile sits at 498 of 512 VGPRs, and the stamps' registers spilled it to
+  // scratch (56-64 B) -- it runs in the 3D filter only, outside the refinement loop's timeline
+  a.clk = nullptr;
   hipLaunchKernelGGL((conv_depth_kernel<17>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, s, a);
   return FSMI_OK;
 }

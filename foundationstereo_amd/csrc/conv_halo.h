@@ -130,6 +130,7 @@ struct HaloArgs {
   // value of output channel co at (d, h, w) is multiplied by sigmoid(fatt[b, co, h, w]),
   // fatt (B, Cout, H, W) contiguous; nullptr: no gate
   const float* fatt;
+  unsigned long long* clk;         // in-kernel launch clock (timer mode 2 / eager timing; nullptr: off)
 };
 
 // Launch conv tile configuration `cfg` (0..9) for kernel size KS, 2D maps or NCDHW volumes
@@ -468,7 +469,14 @@ __device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], i
 // chan() returns a GLOBAL (address space 1) pointer: a pointer rebuilt from an integer is generic,
 // and loads through it were flat_load_dword -- which count in lgkmcnt as well as vmcnt, so every
 // LDS operand wait after a chunk's halo loads also waited for those HBM loads (round 5).
+#ifndef FSMI_HALO_FLAT
+#define FSMI_HALO_FLAT 0                             // 1: the round-4 generic pointers (A/B build only)
+#endif
+#if FSMI_HALO_FLAT
+typedef const float* gcfptr;
+#else
 typedef const __attribute__((address_space(1))) float* gcfptr;
+#endif
 
 struct SegBases {
   uintptr_t p[kHMaxSeg];
@@ -834,6 +842,7 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
 
 template <int KS, int BM, int TR, int WM, bool D3>
 __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
+  ClockScope clk_(a.clk);
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
@@ -1011,6 +1020,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
 // (2r + dh, 2c + dw).
 template <int KS, int BM, int TR, int WM, bool D3, int KG = 1, int STR = 1>
 __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
+  ClockScope clk_(a.clk);
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
@@ -1270,6 +1280,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
 // (65 KB for TR = 4, 109 KB for TR = 8).
 template <int KS, int BM, int TR, int WM>
 __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
+  ClockScope clk_(a.clk);
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;

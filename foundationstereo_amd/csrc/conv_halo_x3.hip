@@ -9,6 +9,7 @@ namespace {
 
 // Sums the split-K partials in split order (deterministic) and applies the epilogue.
 __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
+  ClockScope clk_(a.clk);
   const long long SP = a.cstride;
   const long long n = static_cast<long long>(a.B) * a.Cout * SP;
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
@@ -24,6 +25,7 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
 // Vector form (D*H*W % 4 == 0): one (b, co) channel per blockIdx.y, float4 partial loads, all
 // nsplit of them in flight before the ordered sum.
 __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
+  ClockScope clk_(a.clk);
   const long long SP = a.cstride;
   const long long hw = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 4;
   if (hw >= SP) return;
@@ -73,16 +75,19 @@ namespace fsmi {
 namespace halo {
 
 // the split-K reduce pass of a launch whose partials are in a.ws (also used by conv_lookup.hip)
-void split_reduce(const HaloArgs& a, hipStream_t s) {
+void split_reduce(const HaloArgs& a_in, hipStream_t s) {
+  HaloArgs a = a_in;
   const long long SP = a.cstride;
   const bool vec = SP % 4 == 0 && a.nsplit <= 8 && reinterpret_cast<uintptr_t>(a.out) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(a.ws) % 16 == 0 &&
                    (!a.res || reinterpret_cast<uintptr_t>(a.res) % 16 == 0);
   if (vec) {
-    hipLaunchKernelGGL(conv_split_reduce4_kernel, dim3(static_cast<unsigned>((SP / 4 + 255) / 256), a.B * a.Cout),
-                       dim3(256), 0, s, a);
+    const dim3 grid(static_cast<unsigned>((SP / 4 + 255) / 256), a.B * a.Cout);
+    a.clk = clock_slot(FSMI_K_CONV2D, s, 4ll * grid.x * grid.y, "split_reduce", true);
+    hipLaunchKernelGGL(conv_split_reduce4_kernel, grid, dim3(256), 0, s, a);
   } else {
     const long long n = static_cast<long long>(a.B) * a.Cout * SP;
+    a.clk = clock_slot(FSMI_K_CONV2D, s, 4ll * ((n + 255) / 256), "split_reduce", true);
     hipLaunchKernelGGL(conv_split_reduce_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, a);
   }
 }
@@ -100,6 +105,14 @@ namespace {
 // launches per tile config as launched (0..9 and 11 register / LDS tiles, 10 stride-2, 16 + c K groups,
 // 24..29 pointwise, 30 depth-blocked, 32 + c pipelined): fsmi_conv_launch_counts
 std::atomic<long long> g_cfg_launches[64];
+
+// in-kernel clock slot of a conv launch, tagged with its shape and tile (fsmi_timer_dump_captured)
+unsigned long long* conv_clock(const HaloArgs& a, hipStream_t s, int cfg, int KS, int KD, long long nwaves) {
+  char tag[112];
+  snprintf(tag, sizeof(tag), "conv k%dx%d%s cfg%d ci%d co%d d%d h%d w%d ns%d%s", KD, KS, a.str == 2 ? " s2" : "", cfg,
+           a.Cin, a.Cout, a.D, a.H, a.W, a.nsplit, a.up ? " up" : "");
+  return clock_slot(FSMI_K_CONV2D, s, nwaves, tag, true);
+}
 
 // Shared host side of both entry points: validates, fills HaloArgs (gate fields preset by the
 // caller), picks tiles and split-K, launches.
@@ -258,6 +271,8 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
   }();
   a.dbg = conv_dbg;
   g_cfg_launches[(a.pipe ? 32 : 0) + (kg == 2 ? 16 : 0) + cfg].fetch_add(1, std::memory_order_relaxed);
+  a.clk = conv_clock(a, s, (a.pipe ? 32 : 0) + (kg == 2 ? 16 : 0) + cfg, KS, KD,
+                     4ll * kg * a.npix * a.nco * a.nsplit * (a.up == 2 ? 8 : a.up == 4 ? 4 : 1));
   const int rc = a.str == 2 ? halo::launch_s2(KS, cfg, a, s) : pw ? halo::launch_pw(cfg, a, s) : KS == 2 ? (d3 ? halo::launch_cfg<2, true>(cfg, kg, a, s) : halo::launch_cfg<2, false>(cfg, kg, a, s)) : KS == 3 ? (d3 ? halo::launch_cfg<3, true>(cfg, kg, a, s) : halo::launch_cfg<3, false>(cfg, kg, a, s))
                          : (d3 ? halo::launch_cfg<1, true>(cfg, kg, a, s) : halo::launch_cfg<1, false>(cfg, kg, a, s));
   if (rc != FSMI_OK) return rc;

@@ -42,6 +42,7 @@ struct MlpArgs {
   const float* gamma;              // C or nullptr
   int B, HW, tiles;
   unsigned long long* ts;          // debug (fsmi_debug_conv_timestamps): 8 phase stamps per block
+  unsigned long long* clk;         // in-kernel launch clock (nullptr: off)
 };
 
 // max over the block of per-thread values v >= 0 (8 waves); one barrier
@@ -61,6 +62,7 @@ __device__ __forceinline__ void mlp_stamp(const MlpArgs& a, int k) {
 
 template <int C>
 __global__ __launch_bounds__(512) void edgenext_mlp_kernel(MlpArgs a) {
+  ClockScope clk_(a.clk);
   constexpr int E = 4 * C, PX = kMlpPX;
   constexpr int XR = C + 8, HR = E + 8;            // padded LDS rows (halves): 16-B aligned, 4-bank skew
   constexpr int NKX = C / HKC, NKH = E / HKC;      // 32-channel chunks of x / of the hidden map
@@ -288,6 +290,7 @@ extern "C" int fsmi_edgenext_mlp(const float* x, const float* res, float* out, c
   a.tiles = (a.HW + kMlpPX - 1) / kMlpPX;
   a.ts = g_conv_ts;
   hipStream_t s = as_stream(stream);
+  a.clk = clock_slot(FSMI_K_CONV2D, s, 8ll * B * a.tiles, "edgenext_mlp", true);
   LaunchTimer t(FSMI_K_CONV2D, s);
   hipLaunchKernelGGL(edgenext_mlp_kernel<128>, dim3(static_cast<unsigned>(B * a.tiles)), dim3(512), 0, s, a);
   return finish_launch("fsmi_edgenext_mlp");

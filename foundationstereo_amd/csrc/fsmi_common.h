@@ -41,7 +41,11 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // The host takes max(end) - min(start) per launch; waves that exit early leave a 0 end.
 // nullptr otherwise (graph replays carry no clock).  bench.py divides the roofline bytes by this
 // duration: the kernel's execution time, without the event-record latency around a launch.
-unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves);
+// timeline = true: the launch takes a slot only in timer mode 3 (a whole forward's timeline,
+// fsmi_timer_dump_captured); the geometry kernels (false) take one in modes 1 / 2 as well
+unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves, const char* tag = nullptr,
+                               bool timeline = false);
+
 
 // Replay hook for fsmi_timer_replay: while timing is on (and not capturing), an instrumented
 // entry point registers a closure that re-issues its last launch with identical arguments on the
@@ -72,6 +76,13 @@ __device__ __forceinline__ void clock_end(unsigned long long* slot) {
     if ((threadIdx.x & 63) == 0) slot[2 * clock_wave_id() + 1] = wall_clock64();
   }
 }
+
+// Clock of a kernel whose waves may leave early: the end stamp from the scope's exit (destructor).
+struct ClockScope {
+  unsigned long long* slot;
+  __device__ __forceinline__ explicit ClockScope(unsigned long long* s) : slot(s) { clock_begin(s); }
+  __device__ __forceinline__ ~ClockScope() { clock_end(slot); }
+};
 
 inline int finish_launch(const char* what) {
   hipError_t e = hipGetLastError();

@@ -165,7 +165,8 @@ __global__ __launch_bounds__(256) void normalize_cols_kernel(const float* __rest
 // w1 tile), one wave per w2 tile; each wave streams its two 32-column slabs
 // from L2 (row-major blocks of a row share one XCD) 16 k-steps of loads ahead
 // of the MFMAs that consume them.
-__global__ __launch_bounds__(kCorrMaxT * kWave) void allpairs_corr_direct_kernel(
+template <int MAXT>
+__global__ __launch_bounds__(MAXT * kWave) void allpairs_corr_direct_kernel(
     const float* __restrict__ nl, const float* __restrict__ nr, float* __restrict__ lv0, float* __restrict__ lv1,
     float* __restrict__ lv2, float* __restrict__ lv3, int L, int C, int H, int W, int T, unsigned long long* clk) {
   clock_begin(clk);
@@ -464,8 +465,14 @@ int fsmi_allpairs_corr(const float* fl, const float* fr, float* const* levels, i
     const unsigned ngrid = ceil_div(P, 64), cgrid = static_cast<unsigned>(B) * H * T;
     hipLaunchKernelGGL(normalize_cols_kernel, dim3(ngrid, 2), dim3(64), 0, s, fl, fr, nl, nr, C, H * W, P,
                        clock_slot(FSMI_K_NORM, s, 2ll * ngrid));
-    hipLaunchKernelGGL(allpairs_corr_direct_kernel, dim3(cgrid), dim3(T * kWave), 0, s, nl, nr, lv[0], lv[1], lv[2],
-                       lv[3], num_levels, C, H, W, T, clock_slot(FSMI_K_CORR, s, static_cast<long long>(cgrid) * T));
+    // up to 8 w2 tiles (W <= 256) with a 512-thread bound: 128 VGPRs (the 1024-thread bound) spilled
+    unsigned long long* clk = clock_slot(FSMI_K_CORR, s, static_cast<long long>(cgrid) * T, "allpairs_corr");
+    if (T <= 8)
+      hipLaunchKernelGGL(allpairs_corr_direct_kernel<8>, dim3(cgrid), dim3(T * kWave), 0, s, nl, nr, lv[0], lv[1],
+                         lv[2], lv[3], num_levels, C, H, W, T, clk);
+    else
+      hipLaunchKernelGGL(allpairs_corr_direct_kernel<kCorrMaxT>, dim3(cgrid), dim3(T * kWave), 0, s, nl, nr, lv[0],
+                         lv[1], lv[2], lv[3], num_levels, C, H, W, T, clk);
   } else {
     hipLaunchKernelGGL(allpairs_corr_kernel, dim3(static_cast<unsigned>(B) * H * T), dim3(T * kWave), 0, s,
                        fl, fr, lv[0], lv[1], lv[2], lv[3], num_levels, C, H, W, T);

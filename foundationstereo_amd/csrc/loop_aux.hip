@@ -17,7 +17,9 @@ constexpr int DWK_TR = 32, DWK_RPT = 8;
 template <int KS>
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias, float* __restrict__ out,
-                                                     int C, int H, int W, int ntr, int ntc) {
+                                                     int C, int H, int W, int ntr, int ntc,
+                                                     unsigned long long* clk) {
+  ClockScope clk_(clk);
   constexpr int P = KS / 2, IR = DWK_TR + KS - 1, IC = DW_TC + KS - 1, RPT = DWK_RPT;
   __shared__ float tile[IR][IC + 1];
   const int plane = blockIdx.x / (ntr * ntc);
@@ -69,7 +71,9 @@ constexpr int C1_CO = 8;
 template <int KS>
 __global__ __launch_bounds__(256) void conv_1in_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, float* __restrict__ out,
-                                                       int Cout, int H, int W, int ntr, int ntc, int relu) {
+                                                       int Cout, int H, int W, int ntr, int ntc, int relu,
+                                                       unsigned long long* clk) {
+  ClockScope clk_(clk);
   constexpr int P = KS / 2, IR = DW_TR + KS - 1, IC = DW_TC + KS - 1;
   __shared__ float tile[IR][IC + 1];
   const int b = blockIdx.x / (ntr * ntc);
@@ -113,7 +117,9 @@ __global__ __launch_bounds__(256) void conv_1in_kernel(const float* __restrict__
 // pool2x: F.avg_pool2d(x, 3, stride=2, padding=1) with count_include_pad (every window / 9),
 // core/update.py:72-73.  One thread per output; the 3 input rows are contiguous 3-float runs.
 __global__ __launch_bounds__(256) void pool2x_kernel(const float* __restrict__ x, float* __restrict__ out,
-                                                     int H, int W, int Ho, int Wo, long long n) {
+                                                     int H, int W, int Ho, int Wo, long long n,
+                                                     unsigned long long* clk) {
+  ClockScope clk_(clk);
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= n) return;
   const int ox = static_cast<int>(i % Wo);
@@ -137,8 +143,10 @@ __global__ __launch_bounds__(256) void pool2x_kernel(const float* __restrict__ x
 // F.interpolate(mode="bilinear", align_corners=True): src = dst * (in-1)/(out-1)
 __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x, float* __restrict__ out,
                                                      long long planes, int Hi, int Wi, int Ho, int Wo, float sh,
-                                                     float sw) {
+                                                     float sw,
+                                                     unsigned long long* clk) {
 #pragma clang fp contract(off)
+  ClockScope clk_(clk);
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
   const long long n = planes * Ho * Wo;
   if (i >= n) return;
@@ -170,9 +178,10 @@ extern "C" int fsmi_dwconv2d(const float* x, const float* w, const float* bias, 
   LaunchTimer t(FSMI_K_DWCONV, s);
   const int ntr = (H + DWK_TR - 1) / DWK_TR, ntc = (W + DW_TC - 1) / DW_TC;
   const dim3 grid(static_cast<unsigned>(B) * C * ntr * ntc);
-  if (KS == 7) hipLaunchKernelGGL(dwconv_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
-  else if (KS == 5) hipLaunchKernelGGL(dwconv_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
-  else hipLaunchKernelGGL(dwconv_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc);
+  unsigned long long* clk = clock_slot(FSMI_K_DWCONV, s, 4ll * grid.x * grid.y * grid.z, "dwconv", true);
+  if (KS == 7) hipLaunchKernelGGL(dwconv_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc, clk);
+  else if (KS == 5) hipLaunchKernelGGL(dwconv_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc, clk);
+  else hipLaunchKernelGGL(dwconv_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc, clk);
   return finish_launch("fsmi_dwconv2d");
 }
 
@@ -185,9 +194,10 @@ extern "C" int fsmi_conv2d_1in(const float* x, const float* w, const float* bias
   LaunchTimer t(FSMI_K_DWCONV, s);
   const int ntr = (H + DW_TR - 1) / DW_TR, ntc = (W + DW_TC - 1) / DW_TC;
   const dim3 grid(static_cast<unsigned>(B) * ntr * ntc, (Cout + C1_CO - 1) / C1_CO);
-  if (KS == 7) hipLaunchKernelGGL(conv_1in_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
-  else if (KS == 5) hipLaunchKernelGGL(conv_1in_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
-  else hipLaunchKernelGGL(conv_1in_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu);
+  unsigned long long* clk = clock_slot(FSMI_K_DWCONV, s, 4ll * grid.x * grid.y * grid.z, "conv_1in", true);
+  if (KS == 7) hipLaunchKernelGGL(conv_1in_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu, clk);
+  else if (KS == 5) hipLaunchKernelGGL(conv_1in_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu, clk);
+  else hipLaunchKernelGGL(conv_1in_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, Cout, H, W, ntr, ntc, relu, clk);
   return finish_launch("fsmi_conv2d_1in");
 }
 
@@ -198,7 +208,8 @@ extern "C" int fsmi_pool2x(const float* x, float* out, int B, int C, int H, int 
   LaunchTimer t(FSMI_K_RESIZE, s);
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long long n = static_cast<long long>(B) * C * Ho * Wo;
-  hipLaunchKernelGGL(pool2x_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, x, out, H, W, Ho, Wo, n);
+  hipLaunchKernelGGL(pool2x_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, s, x, out, H, W, Ho, Wo, n,
+                     clock_slot(FSMI_K_RESIZE, s, 4ll * ceil_div(n, 256), "pool2x", true));
   return finish_launch("fsmi_pool2x");
 }
 
@@ -213,6 +224,6 @@ extern "C" int fsmi_resize_bilinear(const float* x, float* out, int B, int C, in
   const long long planes = static_cast<long long>(B) * C;
   const long long n = planes * Ho * Wo;
   hipLaunchKernelGGL(resize_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, x, out, planes,
-                     Hi, Wi, Ho, Wo, sh, sw);
+                     Hi, Wi, Ho, Wo, sh, sw, clock_slot(FSMI_K_RESIZE, s, 4ll * ((n + 255) / 256), "resize", true));
   return finish_launch("fsmi_resize_bilinear");
 }

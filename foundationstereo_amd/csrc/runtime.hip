@@ -1,5 +1,7 @@
 // Library plumbing: thread-local error text, version, live launch timing.
+#include <cstring>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "fsmi_common.h"
@@ -30,7 +32,8 @@ struct Pool {
 };
 std::mutex g_mu;
 bool g_enabled = false;
-bool g_clock_in_capture = false;   // fsmi_timer_enable(2): clock slots also inside stream capture
+bool g_clock_in_capture = false;   // fsmi_timer_enable(2 / 3): clock slots also inside stream capture
+bool g_timeline = false;           // fsmi_timer_enable(3): every instrumented kernel takes a slot
 Pool g_pool[FSMI_K_COUNT];
 
 bool take(int k, hipEvent_t* s, hipEvent_t* e) {
@@ -51,7 +54,7 @@ bool take(int k, hipEvent_t* s, hipEvent_t* e) {
 
 // in-kernel clock: a device arena of per-wave (start, end) stamps, bump-allocated per launch and
 // zeroed at enable / reset; per kernel the host keeps (offset, nwaves) of each launch
-constexpr size_t kClockArena = size_t(1) << 22;       // u64 stamps (32 MB)
+constexpr size_t kClockArena = size_t(1) << 26;       // u64 stamps (512 MB: a timeline of a whole forward)
 unsigned long long* g_clock = nullptr;
 size_t g_clock_top = 0;
 // slots handed to launches captured into a hipGraph (timer mode 2) stay reserved for the life of the
@@ -63,6 +66,15 @@ size_t g_clock_floor = 0;
 // fsmi_timer_release_captured -- the graphs keep rewriting them on every replay)
 std::vector<std::pair<size_t, long long>> g_clock_launch[FSMI_K_COUNT];
 std::vector<std::pair<size_t, long long>> g_clock_captured[FSMI_K_COUNT];
+// every captured launch in capture order, for fsmi_timer_dump_captured (the replay's timeline)
+struct CapRecord {
+  int kernel;
+  size_t off;
+  long long nwaves;
+  const void* stream;
+  std::string tag;
+};
+std::vector<CapRecord> g_clock_caplog;
 // launches that found the arena full, eager (this session) and captured (reported by the queries)
 long long g_clock_dropped[FSMI_K_COUNT], g_clock_dropped_cap[FSMI_K_COUNT];
 
@@ -80,8 +92,8 @@ static int clock_init() {
   return FSMI_OK;
 }
 
-unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves) {
-  if (!g_enabled || !g_clock || nwaves <= 0) return nullptr;
+unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves, const char* tag, bool timeline) {
+  if (!g_enabled || !g_clock || nwaves <= 0 || (timeline && !g_timeline)) return nullptr;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &st) != hipSuccess) return nullptr;
   // inside a capture the slot pointer is baked into the graph node: every replay overwrites the same
@@ -96,6 +108,7 @@ unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves)
     return nullptr;
   }
   (captured ? g_clock_captured : g_clock_launch)[kernel].emplace_back(g_clock_top, nwaves);
+  if (captured) g_clock_caplog.push_back({kernel, g_clock_top, nwaves, stream, tag ? tag : ""});
   unsigned long long* p = g_clock + g_clock_top;
   g_clock_top += need;
   if (captured) g_clock_floor = g_clock_top;   // baked into a graph: reserved
@@ -182,7 +195,8 @@ const char* fsmi_arch(void) { return "gfx950"; }
 int fsmi_timer_enable(int on) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   fsmi::g_enabled = on != 0;
-  fsmi::g_clock_in_capture = on == 2;
+  fsmi::g_clock_in_capture = on >= 2;
+  fsmi::g_timeline = on == 3;
   for (auto& f : fsmi::g_replay) f = nullptr;      // a replay only targets buffers of the current session
   if (fsmi::g_enabled) {
     if (fsmi::clock_init() != FSMI_OK) {
@@ -333,9 +347,46 @@ int fsmi_timer_query_clock_captured(int kernel, double* total_ms, long long* cou
   return query_clock(fsmi::g_clock_captured[kernel], total_ms, count);
 }
 
+int fsmi_timer_dump_captured(char* buf, long long size, long long* needed) {
+  std::lock_guard<std::mutex> lk(fsmi::g_mu);
+  std::string text;
+  if (!fsmi::g_clock_caplog.empty()) {
+    hipError_t e = hipDeviceSynchronize();
+    std::vector<unsigned long long> v;
+    char line[96];
+    for (const auto& r : fsmi::g_clock_caplog) {
+      v.resize(2 * static_cast<size_t>(r.nwaves));
+      if (e == hipSuccess)
+        e = hipMemcpy(v.data(), fsmi::g_clock + r.off, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        fsmi::set_error("fsmi_timer_dump_captured: %s", hipGetErrorString(e));
+        return static_cast<int>(e);
+      }
+      unsigned long long t0 = ~0ULL, t1 = 0;
+      for (size_t i = 0; i < v.size(); i += 2) {
+        if (v[i]) t0 = std::min(t0, v[i]);
+        t1 = std::max(t1, v[i + 1]);
+      }
+      if (t0 == ~0ULL) t0 = 0;
+      snprintf(line, sizeof(line), "%d %p %llu %llu ", r.kernel, r.stream, t0, t1);
+      text += line;
+      text += r.tag;
+      text += "\n";
+    }
+  }
+  if (needed) *needed = static_cast<long long>(text.size()) + 1;
+  if (buf && size > 0) {
+    const size_t n = std::min(text.size(), static_cast<size_t>(size - 1));
+    memcpy(buf, text.data(), n);
+    buf[n] = 0;
+  }
+  return FSMI_OK;
+}
+
 int fsmi_timer_release_captured(void) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   for (auto& v : fsmi::g_clock_captured) v.clear();
+  fsmi::g_clock_caplog.clear();
   for (auto& d : fsmi::g_clock_dropped_cap) d = 0;
   fsmi::g_clock_floor = 0;
   fsmi::g_clock_top = 0;

@@ -909,10 +909,13 @@ def _keep_for_replay(kernel: str, *tensors):
         _REPLAY_KEEP[kernel] = tensors
 
 
-def timer_enable(on: bool = True, in_capture: bool = False):
-    """Per-kernel timers on / off.  ``in_capture``: the lookup / build kernel clocks are also baked
-    into launches captured into a hipGraph (each replay rewrites them; query after replaying)."""
-    _lib.check(_lib.load().fsmi_timer_enable((2 if in_capture else 1) if on else 0), "timer_enable")
+def timer_enable(on: bool = True, in_capture: bool = False, timeline: bool = False):
+    """Per-kernel timers on / off.  ``in_capture``: the geometry kernels' clocks are also baked into
+    launches captured into a hipGraph (each replay rewrites them; query after replaying).
+    ``timeline``: every instrumented kernel (convs, MLP, aux) is clocked in the capture as well
+    (timer mode 3; ``timer_dump_captured``)."""
+    mode = (3 if timeline else 2 if in_capture else 1) if on else 0
+    _lib.check(_lib.load().fsmi_timer_enable(mode), "timer_enable")
     _CONV_FLOPS["on"] = bool(on)
     _REPLAY_KEEP.clear()
 
@@ -952,6 +955,23 @@ def timer_query_clock(kernel: str, captured: bool = False):
     fn = _lib.load().fsmi_timer_query_clock_captured if captured else _lib.load().fsmi_timer_query_clock
     _lib.check(fn(_lib.KERNELS.index(kernel), ctypes.byref(tot), ctypes.byref(cnt)), "timer_query_clock")
     return tot.value, cnt.value
+
+
+def timer_dump_captured():
+    """[(kernel, stream handle, start tick, end tick, tag)] of every launch captured with clocks, in
+    capture order (include/fsmi.h fsmi_timer_dump_captured; ticks of 10 ns)."""
+    import ctypes
+    lib = _lib.load()
+    need = ctypes.c_longlong(0)
+    _lib.check(lib.fsmi_timer_dump_captured(None, 0, ctypes.byref(need)), "timer_dump_captured")
+    buf = ctypes.create_string_buffer(int(need.value))
+    _lib.check(lib.fsmi_timer_dump_captured(buf, need.value, ctypes.byref(need)), "timer_dump_captured")
+    out = []
+    for line in buf.value.decode().splitlines():
+        k, st, t0, t1, *tag = line.split(" ", 4)
+        out.append((int(k), int(st, 16) if st.startswith("0x") else 0, int(t0), int(t1),
+                    (tag[0] if tag else "").strip()))
+    return out
 
 
 def timer_release_captured():

@@ -35,6 +35,9 @@ FUSED_GATES = os.environ.get("FSMI_FUSED_GATES", "1") != "0"
 # PIPE_BRANCH: gru04's small branch on its own stream there
 PIPELINE = os.environ.get("FSMI_PIPELINE", "1") != "0"
 PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
+# run_pipelined: the disparity head of iteration t enqueued (captured) BEFORE gru08(t+1), which then
+# waits on an event recorded after gru04(t) instead of on the whole main stream (A/B knob)
+HEAD_FIRST = os.environ.get("FSMI_HEAD_FIRST", "0") != "0"
 
 
 # the disparity head writes disp + delta into the next encoder buffer (A/B knob)
@@ -463,6 +466,19 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             _BRANCH[0] = 1 if main_branch else 0
             n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0))
             _BRANCH[0] = 1
+            if HEAD_FIRST and HEAD_INPLACE and t + 1 < iters:
+                ev04 = torch.cuda.Event()
+                ev04.record(main)                        # gru04(t) done: gru08(t+1) needs nothing else
+                enc = disp.new_empty(B, nc + 1, H, W)
+                self.disp_head(n0, res=disp, out=enc, co0=nc)
+                disp = enc[:, nc:]
+                s_gru.wait_event(ev04)
+                _BRANCH[0] = 0
+                with torch.cuda.stream(s_gru):           # gru08(t+1), beside the next motion path
+                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
+                _BRANCH[0] = 1
+                main.wait_stream(s_mot)
+                continue
             if t + 1 < iters:
                 s_gru.wait_stream(main)                  # gru04(t)
                 # both branches in order: forking gru08's 1x1 branch to the (then idle) branch stream

@@ -339,7 +339,8 @@ int fsmi_get_range_safe(int* safe);
 
 /* on: 0 off, 1 on (events + kernel clocks outside stream capture), 2 also the kernel clocks of
  * launches captured into a hipGraph (their stamps are rewritten by every replay: a query after the
- * replays reads the last replay's launches -- bench.py's in-step lookup timing). */
+ * replays reads the last replay's launches -- bench.py's in-step lookup timing), 3 as 2 with every
+ * instrumented kernel clocked, not only the geometry kernels (fsmi_timer_dump_captured). */
 int fsmi_timer_enable(int on);
 int fsmi_timer_reset(void);
 int fsmi_timer_query(int kernel, double* total_ms, long long* count);
@@ -356,6 +357,12 @@ int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count);
  * (FSMI_ERR_ARG) when a launch of the kernel found the 4M-stamp clock arena full. */
 int fsmi_timer_query_clock_captured(int kernel, double* total_ms, long long* count);
 int fsmi_timer_release_captured(void);
+/* The replay's timeline: one text line per launch captured in timer mode 2, in capture order,
+ * "<kernel id> <stream> <first wave start> <last wave end> <tag>" (s_memrealtime ticks, 100 MHz;
+ * 0 0 for a launch no replay has run).  Writes at most size bytes (NUL-terminated); *needed = the
+ * full length + 1.  Instrumented: the halo / pointwise conv kernels and their split-K reduce, the
+ * EdgeNeXt MLP, depthwise / 1-input convs, pool / resize, and the geometry kernels. */
+int fsmi_timer_dump_captured(char* buf, long long size, long long* needed);
 /* Re-issue the last timed launch of `kernel` (lookup, cost-volume build) `reps` times back to
  * back on its stream between two hipEvents; *avg_ms = span / reps.  The kernels are pure
  * functions of their inputs, so the replays rewrite identical outputs.

@@ -25,20 +25,37 @@ def test_lookup_clock_in_captured_graph():
         with torch.cuda.graph(g):
             out = ops.geo_lookup(pyr, corr, disp, 4)
             out2 = ops.geo_lookup(pyr, corr, disp, 4)
+            corr_g = ops.allpairs_corr(f1, f2, L)
+            pyr_g = ops.volume_pyramid(vol, L)
         ops.timer_enable(False)
         for _ in range(3):
             g.replay()
         torch.cuda.synchronize()
-        ms, n = ops.timer_query_clock("lookup")
+        ms, n = ops.timer_query_clock("lookup", captured=True)
         assert n == 2 and 0.0 < ms / n < 5.0, (ms, n)       # both captured launches stamped, sane us
+        assert ops.timer_query_clock("lookup")[1] == 0       # no eager launch since the enable
+        for k in ("corr", "norm", "volpyr"):                 # the other geometry kernels' in-step clocks
+            ms, n = ops.timer_query_clock(k, captured=True)
+            assert n == 1 and 0.0 < ms < 5.0, (k, ms, n)
         assert torch.equal(out, ref) and torch.equal(out2, ref)
-        # mode 1: captured launches carry no clock
+        for a_, b_ in zip(corr_g + pyr_g[1:], corr + pyr[1:]):
+            assert torch.equal(a_, b_)
+        # mode 1: captured launches carry no clock; the records of the mode-2 graph survive the
+        # new session (its replays keep writing those slots), until released
         ops.timer_enable(True)
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2):
             ops.geo_lookup(pyr, corr, disp, 4)
         g2.replay()
+        ops.geo_lookup(pyr, corr, disp, 4)                   # one eager launch: clocked in mode 1
         torch.cuda.synchronize()
-        assert ops.timer_query_clock("lookup")[1] == 0
+        assert ops.timer_query_clock("lookup")[1] == 1
+        assert ops.timer_query_clock("lookup", captured=True)[1] == 2
+        g.replay()
+        torch.cuda.synchronize()
+        assert ops.timer_query_clock("lookup", captured=True)[1] == 2
+        del g
+        ops.timer_release_captured()
+        assert ops.timer_query_clock("lookup", captured=True)[1] == 0
     finally:
         ops.timer_enable(False)

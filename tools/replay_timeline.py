@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Timeline of the graph-replayed forward WITHOUT a profiler: every instrumented kernel of the captured
+forward stamps its first wave start and last wave end (s_memrealtime, 10 ns) into a slot baked into the
+graph (timer mode 2, include/fsmi.h fsmi_timer_dump_captured); after the replays the last replay's
+stamps are read back.  rocprofv3's kernel trace re-maps the graph onto its own hardware queues and
+slows the step (~17 vs ~21 pairs/s at cfg2), so its per-iteration picture is not the timed step's.
+
+    python tools/replay_timeline.py [--config cfg2] [--iter 16] [--out gpurun_out/r5/replay_timeline.txt]
+
+Prints, for iteration ``--iter`` (lookup(t) start .. lookup(t+1) start): every stamped launch with its
+capture stream (main / motion / branch / pipeline), start / end in us from lookup(t), duration and tag;
+the busy time per stream; and the chain that sets the iteration's length (from lookup(t+1) back, each
+step the launch that finished last before the current one started).  Kernels without a clock (the
+few non-fsmi ops, MIOpen) are absent, so gaps in the chain can hide them.  Also the whole step: span,
+kernel time per stream and the sum over launches per tag family.
+"""
+import argparse
+import json
+import os
+import re
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from foundationstereo_amd import _lib, ops, synth  # noqa: E402
+from foundationstereo_amd import update as fupdate  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="cfg2")
+ap.add_argument("--iter", type=int, default=16)
+ap.add_argument("--replays", type=int, default=5)
+ap.add_argument("--out", default="")
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+H, W, md, iters, vit, per = bench.CONFIGS[a.config]
+args = synth.make_args(max_disp=md, corr_levels=4, vit_size=vit)
+model = bench.make_model(args, dev, 0)
+feats = [synth.backbone_features(1, H, W, vit, seed=0x5EED + i, shift_px=8) for i in range(per)]
+fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(dev) for j in range(4)]
+fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(dev) for j in range(4)]
+vf = torch.from_numpy(np.concatenate([f[2] for f in feats])).to(dev)
+model.feature.set_features(fl, fr, vf, size=(H, W))
+left, right = synth.stereo_images(per, H, W)
+L, R = torch.from_numpy(left).to(dev), torch.from_numpy(right).to(dev)
+lib = _lib.load()
+with torch.no_grad():
+    for _ in range(2):
+        model(L, R, iters=iters, test_mode=True)
+    torch.cuda.synchronize()
+    ops.timer_enable(True, timeline=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        model(L, R, iters=iters, test_mode=True)
+    ops.timer_enable(False)
+for _ in range(a.replays):
+    g.replay()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+g.replay()
+e1.record()
+torch.cuda.synchronize()
+step_ms = e0.elapsed_time(e1)
+names = {}
+for idx, nm in ((0, "motion"), (1, "branch"), (3, "pipeline")):
+    names[fupdate._side_stream(dev, idx).cuda_stream] = nm
+recs = [{"k": k, "stream": names.get(sp, "main"), "s": t0, "e": t1, "tag": tag or _lib.KERNELS[k]}
+        for k, sp, t0, t1, tag in ops.timer_dump_captured()]
+recs = [r for r in recs if r["s"] and r["e"] >= r["s"]]
+recs.sort(key=lambda r: r["s"])
+out = []
+
+
+def emit(x=""):
+    out.append(x)
+    print(x)
+
+
+t_first, t_last = recs[0]["s"], max(r["e"] for r in recs)
+emit(f"{a.config}: replay device time {step_ms:.2f} ms (events); stamped span {(t_last - t_first) / 1e5:.2f} ms, "
+     f"{len(recs)} stamped launches")
+per_stream = {}
+for r in recs:
+    per_stream[r["stream"]] = per_stream.get(r["stream"], 0) + r["e"] - r["s"]
+emit("kernel time per stream (whole step): " + ", ".join(f"{k} {v / 1e5:.2f} ms" for k, v in sorted(per_stream.items())))
+fam = {}
+for r in recs:
+    f = re.sub(r" (ci|co|d|h|w|ns)\d+", "", r["tag"])
+    fam[f] = fam.get(f, 0) + r["e"] - r["s"]
+emit("top launch families (summed kernel time, ms): " + json.dumps(
+    {k: round(v / 1e5, 2) for k, v in sorted(fam.items(), key=lambda x: -x[1])[:12]}))
+lk = [i for i, r in enumerate(recs) if r["k"] == _lib.KERNELS.index("lookup")]
+if len(lk) > a.iter + 1:
+    first, nxt = recs[lk[a.iter]], recs[lk[a.iter + 1]]
+    t0, t1 = first["s"], nxt["s"]
+    sel = [r for r in recs if r["e"] > t0 and r["s"] < t1]
+    emit(f"iteration {a.iter}: {(t1 - t0) / 100:.1f} us lookup to lookup, {len(sel)} stamped launches")
+    for r in sel:
+        emit(f"  {r['stream']:>8} {(r['s'] - t0) / 100:8.1f} {(r['e'] - t0) / 100:8.1f} {(r['e'] - r['s']) / 100:7.1f}  {r['tag']}")
+    busy = {}
+    for r in sel:
+        busy[r["stream"]] = busy.get(r["stream"], 0) + min(r["e"], t1) - max(r["s"], t0)
+    emit("  busy per stream: " + ", ".join(f"{k} {v / 100:.0f} us ({v / (t1 - t0):.0%})" for k, v in sorted(busy.items())))
+    chain, cur = [nxt], nxt
+    while True:
+        cands = [r for r in recs if r["e"] <= cur["s"] and r["e"] > t0 and r is not cur]
+        if not cands:
+            break
+        p = max(cands, key=lambda r: r["e"])
+        chain.append(p)
+        if p is first or p["s"] <= t0:
+            break
+        cur = p
+    chain.reverse()
+    ktime = sum(r["e"] - r["s"] for r in chain if r["s"] >= t0 and r is not nxt)
+    emit(f"  critical chain: {len(chain)} launches, {ktime / 100:.0f} us of kernels + "
+         f"{(t1 - t0 - ktime) / 100:.0f} us between them (gaps, unstamped kernels)")
+    for r in chain:
+        emit(f"    {r['stream']:>8} {(r['s'] - t0) / 100:8.1f} {(r['e'] - t0) / 100:8.1f} {(r['e'] - r['s']) / 100:7.1f}  {r['tag']}")
+if a.out:
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        f.write("\n".join(out) + "\n")
