@@ -111,8 +111,8 @@ def load():
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name, None)
-        if fn is None and name.startswith("fsmi_debug_"):   # debug hooks absent from an older A/B build
-            continue
+        if fn is None and (name.startswith("fsmi_debug_") or name == "fsmi_timer_dump_captured"):
+            continue                     # diagnostics absent from an older A/B build (FSMI_LIB)
         if fn is None:
             raise FsmiError(f"{path}: missing symbol {name}")
         fn.argtypes = argtypes

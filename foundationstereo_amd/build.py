@@ -80,6 +80,12 @@ def build_library(force: bool = False, verbose: bool = False, defines=(), varian
     return lib
 
 
+def build_timeline(force: bool = False, verbose: bool = False) -> str:
+    """The diagnostic build whose conv / MLP / aux kernels stamp in-kernel clocks in timer mode 3
+    (_lib/libfsmi_timeline.so, tools/replay_timeline.py); not built by __graft_entry__.build()."""
+    return build_library(force=force, verbose=verbose, defines=("FSMI_TIMELINE=1",), variant="timeline")
+
+
 def build_fast(force: bool = False, verbose: bool = False) -> str:
     """The reference-precision library (one fp16 MFMA product per MAC), _lib/libfsmi_fast.so."""
     return build_library(force=force, verbose=verbose, defines=FAST_DEFINES, variant="fast")

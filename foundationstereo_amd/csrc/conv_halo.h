@@ -842,7 +842,7 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
 
 template <int KS, int BM, int TR, int WM, bool D3>
 __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(256) void conv_halo_x3_kernel(HaloArgs a) {
 // (2r + dh, 2c + dw).
 template <int KS, int BM, int TR, int WM, bool D3, int KG = 1, int STR = 1>
 __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;
@@ -1280,7 +1280,7 @@ __global__ __launch_bounds__(256 * KG) void conv_halo_wreg_kernel(HaloArgs a) {
 // (65 KB for TR = 4, 109 KB for TR = 8).
 template <int KS, int BM, int TR, int WM>
 __global__ __launch_bounds__(256) void conv_halo_pipe_kernel(HaloArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM / 32, TN = TR / WN;
   constexpr int NTAP = KS * KS;

@@ -9,7 +9,7 @@ namespace {
 
 // Sums the split-K partials in split order (deterministic) and applies the epilogue.
 __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   const long long SP = a.cstride;
   const long long n = static_cast<long long>(a.B) * a.Cout * SP;
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void conv_split_reduce_kernel(HaloArgs a) {
 // Vector form (D*H*W % 4 == 0): one (b, co) channel per blockIdx.y, float4 partial loads, all
 // nsplit of them in flight before the ordered sum.
 __global__ __launch_bounds__(256) void conv_split_reduce4_kernel(HaloArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   const long long SP = a.cstride;
   const long long hw = (static_cast<long long>(blockIdx.x) * 256 + threadIdx.x) * 4;
   if (hw >= SP) return;

@@ -67,7 +67,7 @@ __device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); 
 // another's MFMAs.
 template <int BM, int PX, int WM, int NS, bool COOP = false>
 __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   constexpr int WN = 4 / WM, TM = BM / WM / 32, TN = PX / WN / 32;
   constexpr int CHF = HKC * PX;                    // floats per chunk: 32 channel rows x PX pixels
   constexpr int OPS = CHF / (4 * 256);             // DMA instructions per wave per chunk (16 B a lane)

@@ -62,7 +62,7 @@ __device__ __forceinline__ void mlp_stamp(const MlpArgs& a, int k) {
 
 template <int C>
 __global__ __launch_bounds__(512) void edgenext_mlp_kernel(MlpArgs a) {
-  ClockScope clk_(a.clk);
+  FSMI_TIMELINE_CLOCK(a.clk);
   constexpr int E = 4 * C, PX = kMlpPX;
   constexpr int XR = C + 8, HR = E + 8;            // padded LDS rows (halves): 16-B aligned, 4-bank skew
   constexpr int NKX = C / HKC, NKH = E / HKC;      // 32-channel chunks of x / of the hidden map

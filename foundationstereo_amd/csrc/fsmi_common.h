@@ -63,17 +63,23 @@ int* range_flag_device();
 // one fixed from the first nonzero chunk; read when a launch's arguments are built.
 int range_safe();
 
-__device__ __forceinline__ long long clock_wave_id() {
-  const long long blk = blockIdx.x + static_cast<long long>(gridDim.x) * (blockIdx.y + static_cast<long long>(gridDim.y) * blockIdx.z);
-  return blk * ((blockDim.x * blockDim.y * blockDim.z + 63) / 64) + (threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z)) / 64;
+// the wave's slot index, wave-uniform (readfirstlane: SGPRs, so a value the compiler keeps from the
+// begin stamp to the end stamp costs the main loop no VGPR -- the per-lane form cost the conv tiles
+// 5-20 VGPRs and the cfg2 step 5 %, round 5)
+__device__ __forceinline__ unsigned clock_wave_id() {
+  const unsigned blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const unsigned wpb = (blockDim.x * blockDim.y * blockDim.z + 63) / 64;
+  const unsigned w = __builtin_amdgcn_readfirstlane((threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z)) / 64);
+  return __builtin_amdgcn_readfirstlane(blk * wpb + w);
 }
+// every lane of the wave stores the same stamp to the same slot (one vector store, no lane predicate)
 __device__ __forceinline__ void clock_begin(unsigned long long* slot) {
-  if (slot && (threadIdx.x & 63) == 0) slot[2 * clock_wave_id()] = wall_clock64();
+  if (slot) slot[2 * static_cast<size_t>(clock_wave_id())] = wall_clock64();
 }
 __device__ __forceinline__ void clock_end(unsigned long long* slot) {
   if (slot) {
     __builtin_amdgcn_s_waitcnt(0);
-    if ((threadIdx.x & 63) == 0) slot[2 * clock_wave_id() + 1] = wall_clock64();
+    slot[2 * static_cast<size_t>(clock_wave_id()) + 1] = wall_clock64();
   }
 }
 
@@ -83,6 +89,19 @@ struct ClockScope {
   __device__ __forceinline__ explicit ClockScope(unsigned long long* s) : slot(s) { clock_begin(s); }
   __device__ __forceinline__ ~ClockScope() { clock_end(slot); }
 };
+
+// The conv / pointwise / MLP / aux kernels stamp their clocks only in the timeline build
+// (FSMI_TIMELINE=1, _lib/libfsmi_timeline.so for tools/replay_timeline.py): even a disabled stamp kept
+// the slot pointer and the wave id live through the main loops and cost the cfg2 step 5 % (round 5).
+// The geometry kernels (build, all-pairs, pyramid, lookup) stamp in every build (bench.py's roofline).
+#ifndef FSMI_TIMELINE
+#define FSMI_TIMELINE 0
+#endif
+#if FSMI_TIMELINE
+#define FSMI_TIMELINE_CLOCK(slot) ClockScope fsmi_clock_scope_(slot)
+#else
+#define FSMI_TIMELINE_CLOCK(slot) (void)(slot)
+#endif
 
 inline int finish_launch(const char* what) {
   hipError_t e = hipGetLastError();

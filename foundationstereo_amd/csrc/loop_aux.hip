@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
                                                      const float* __restrict__ bias, float* __restrict__ out,
                                                      int C, int H, int W, int ntr, int ntc,
                                                      unsigned long long* clk) {
-  ClockScope clk_(clk);
+  FSMI_TIMELINE_CLOCK(clk);
   constexpr int P = KS / 2, IR = DWK_TR + KS - 1, IC = DW_TC + KS - 1, RPT = DWK_RPT;
   __shared__ float tile[IR][IC + 1];
   const int plane = blockIdx.x / (ntr * ntc);
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void conv_1in_kernel(const float* __restrict__
                                                        const float* __restrict__ bias, float* __restrict__ out,
                                                        int Cout, int H, int W, int ntr, int ntc, int relu,
                                                        unsigned long long* clk) {
-  ClockScope clk_(clk);
+  FSMI_TIMELINE_CLOCK(clk);
   constexpr int P = KS / 2, IR = DW_TR + KS - 1, IC = DW_TC + KS - 1;
   __shared__ float tile[IR][IC + 1];
   const int b = blockIdx.x / (ntr * ntc);
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void conv_1in_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void pool2x_kernel(const float* __restrict__ x, float* __restrict__ out,
                                                      int H, int W, int Ho, int Wo, long long n,
                                                      unsigned long long* clk) {
-  ClockScope clk_(clk);
+  FSMI_TIMELINE_CLOCK(clk);
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= n) return;
   const int ox = static_cast<int>(i % Wo);
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x
                                                      float sw,
                                                      unsigned long long* clk) {
 #pragma clang fp contract(off)
-  ClockScope clk_(clk);
+  FSMI_TIMELINE_CLOCK(clk);
   const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
   const long long n = planes * Ho * Wo;
   if (i >= n) return;

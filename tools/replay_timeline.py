@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timeline of the graph-replayed forward WITHOUT a profiler: every instrumented kernel of the captured
 forward stamps its first wave start and last wave end (s_memrealtime, 10 ns) into a slot baked into the
-graph (timer mode 2, include/fsmi.h fsmi_timer_dump_captured); after the replays the last replay's
+graph (timer mode 3, include/fsmi.h fsmi_timer_dump_captured; the timeline build _lib/libfsmi_timeline.so,
+whose kernels carry the stamps -- the product build compiles them out); after the replays the last replay's
 stamps are read back.  rocprofv3's kernel trace re-maps the graph onto its own hardware queues and
 slows the step (~17 vs ~21 pairs/s at cfg2), so its per-iteration picture is not the timed step's.
 
@@ -22,6 +23,9 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+# the conv / MLP / aux kernels carry clocks only in the timeline build (python -c "from
+# foundationstereo_amd import build; build.build_timeline()")
+os.environ.setdefault("FSMI_LIB", os.path.join(REPO, "foundationstereo_amd", "_lib", "libfsmi_timeline.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
