@@ -38,6 +38,9 @@ PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 # run_pipelined: the disparity head of iteration t enqueued (captured) BEFORE gru08(t+1), which then
 # waits on an event recorded after gru04(t) instead of on the whole main stream (A/B knob)
 HEAD_FIRST = os.environ.get("FSMI_HEAD_FIRST", "0") != "0"
+# run_pipelined: the motion encoder's disparity branch (convd1, convd2) on the branch stream, beside the
+# lookup and convc1 / convc2 (A/B knob)
+MOTION_FORK = os.environ.get("FSMI_MOTION_FORK", "0") != "0"
 
 
 # the disparity head writes disp + delta into the next encoder buffer (A/B knob)
@@ -92,9 +95,17 @@ def _side_stream(device, idx=0):
     return s
 
 
+# capture_fork -- the rule every fork / join of a side stream here follows under hipGraph capture:
+# a side stream waits only on the capture's origin stream (or on a stream that never waits on it in
+# turn); it may be waited on by any stream, and is joined back by the origin.  On this ROCm (HIP 7,
+# torch 2.10) a side stream X that waits on side stream A which later waits on X (a fork from a side
+# stream plus its join) makes hipStreamEndCapture segfault: tools/capture_fork_probe.py reproduces it
+# with plain torch ops (variants a_only, two_parents, enter_main_wait_side segfault; main_only,
+# via_main pass).  Hence gru08's small branch on the pipeline stream runs in order, and the motion
+# path's disparity branch forks from main, not from the motion stream.
+#
 # side stream the SelectiveConvGRU small branch forks to (1); 0: the branches run in order on the
-# caller's stream (run_pipelined, whose capture must stay within the box's GPU_MAX_HW_QUEUES = 4
-# streams: a capture spread over more crashed hipGraph instantiation)
+# caller's stream (run_pipelined: the pipeline stream is itself a side stream, see capture_fork)
 _BRANCH = [1]
 # run_pipelined: gru08(t+1)'s interp(gru16(t+1)) enqueued right after gru16(t+1), beside gru04(t)
 # (FSMI_EARLY_INTERP=0: after gru04(t), as the reference orders it)
@@ -188,17 +199,34 @@ class BasicMotionEncoder(nn.Module):
         """Writes cat([relu(conv(...)), disp]) into ``out`` (B, 128, H, W) without the cat copy."""
         return self._encode_rest(disp, _conv(self.convc1, [corr], "relu"), out)
 
-    def motion_into(self, disp, geo_fn, out):
-        """The motion path of one iteration: the lookup ``geo_fn(disp)`` and this encoder."""
-        return self.encode_into(disp, geo_fn(disp), out)
+    def motion_into(self, disp, geo_fn, out, fork=None):
+        """The motion path of one iteration: the lookup ``geo_fn(disp)`` and this encoder.  ``fork``:
+        a stream the disparity branch (convd1, convd2 -- they read only ``disp``) runs on, beside the
+        lookup and the correlation branch.  The caller has made ``fork`` wait for ``disp`` (from the
+        capture's origin stream, see ``capture_fork``) and joins it later; its output is allocated
+        on the calling stream, which waits for ``fork`` before the last conv."""
+        if fork is None:
+            return self.encode_into(disp, geo_fn(disp), out)
+        B, _, H, W = disp.shape
+        d = disp.new_empty(B, self.convd2.out_channels, H, W)
+        with torch.cuda.stream(fork):
+            self._disp_feat(disp, d)
+        c1 = _conv(self.convc1, [geo_fn(disp)], "relu")
+        return self._encode_rest(disp, c1, out, d=d, join=fork)
 
-    def _encode_rest(self, disp, c1, out):
-        c = _conv(self.convc2, [c1], "relu")
+    def _disp_feat(self, disp, out=None):
         if _CONVD1_MIOPEN:                                     # A/B knob: the MIOpen conv + ReLU
             d = F.relu_(self.convd1(disp))
         else:
             d = ops.conv2d_1in(disp, self.convd1.weight, self.convd1.bias, relu=True)   # 7x7, 1 -> 64
-        d = _conv(self.convd2, [d], "relu")
+        return _conv(self.convd2, [d], "relu", out=out)
+
+    def _encode_rest(self, disp, c1, out, d=None, join=None):
+        c = _conv(self.convc2, [c1], "relu")
+        if d is None:
+            d = self._disp_feat(disp)
+        if join is not None:
+            torch.cuda.current_stream(disp.device).wait_stream(join)
         # cat([cor, dsp]) with the disparity features (~disp magnitude: ~200 at cfg5) as the FIRST
         # segment: the halo conv fixes a block's exponent from its first chunk (conv_halo.h)
         nc, nd = c.shape[1], d.shape[1]
@@ -451,8 +479,11 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             if not HEAD_INPLACE and t:
                 enc = disp.new_empty(B, nc + 1, H, W)
             s_mot.wait_stream(main)
+            fork = _side_stream(dev, 1) if MOTION_FORK else None
+            if fork is not None:
+                fork.wait_stream(main)                   # forked from the origin (capture_fork)
             with torch.cuda.stream(s_mot):
-                self.encoder.motion_into(disp, geo_fn, enc)
+                self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
             main.wait_stream(s_gru)                      # gru08(t): enqueued last on s_gru so far
             main.wait_stream(s_mot)                      # motion(t)
             if t + 1 < iters:
@@ -481,8 +512,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 continue
             if t + 1 < iters:
                 s_gru.wait_stream(main)                  # gru04(t)
-                # both branches in order: forking gru08's 1x1 branch to the (then idle) branch stream
-                # crashed the process under capture (segfault, round 4)
+                # gru08's branches in order on the pipeline stream: a fork from it would be a side
+                # stream waiting on the pipeline stream and waited on by it (capture_fork)
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru08(t+1), beside the heads + motion(t+1)
                     n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
@@ -502,6 +533,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             else:
                 disp = disp + self.disp_head(n0).float()
             main.wait_stream(s_mot)
+            if fork is not None:
+                main.wait_stream(fork)
         main.wait_stream(s_gru)
         return [n0, n1, n2], mask, disp
 
