@@ -45,6 +45,48 @@ struct MlpArgs {
   unsigned long long* clk;         // in-kernel launch clock (nullptr: off)
 };
 
+// gelu_erf_h (conv_halo.h, FSMI_GELU_FAST) on two values at once: the same operations in the same
+// order on <2 x float>, so the fma / mul / add chains issue as packed v_pk_* instructions (two per
+// lane per issue) and every result is bit-identical to the scalar form.  The GELU of the 4C x 64
+// hidden tile is the kernel's largest VALU phase (~30 operations per element, more issue cycles per
+// block than its MFMAs).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 gelu_erf_h2(f32x2 x) {
+#if FSMI_GELU_FAST
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 t = z * z;
+  f32x2 p = 7.847259258e-05f;
+  p = fma2(p, t, -8.008189034e-04f);
+  p = fma2(p, t, 5.188099109e-03f);
+  p = fma2(p, t, -2.685369179e-02f);
+  p = fma2(p, t, 1.128358245e-01f);
+  p = fma2(p, t, -3.761262596e-01f);
+  p = fma2(p, t, 1.128379107e+00f);
+  const f32x2 small = z * p;
+  const f32x2 az = {fminf(fabsf(z.x), 4.f), fminf(fabsf(z.y), 4.f)};
+  f32x2 r = 1.498133884e-06f;
+  r = fma2(r, az, -4.378752783e-05f);
+  r = fma2(r, az, 5.791864241e-04f);
+  r = fma2(r, az, -4.594380967e-03f);
+  r = fma2(r, az, 2.443690039e-02f);
+  r = fma2(r, az, -9.241911769e-02f);
+  r = fma2(r, az, 2.575692832e-01f);
+  r = fma2(r, az, -5.418152213e-01f);
+  r = fma2(r, az, 8.737412691e-01f);
+  r = fma2(r, az, -1.082139969e+00f);
+  r = fma2(r, az, 9.922678471e-01f);
+  const f32x2 m = -t * 1.4426950408889634f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(m.x), __builtin_amdgcn_exp2f(m.y)};
+  const f32x2 g = fma2(-e, r, 1.f);
+  const f32x2 big = {copysignf(g.x, z.x), copysignf(g.y, z.y)};
+  const f32x2 erf = {fabsf(z.x) < 1.f ? small.x : big.x, fabsf(z.y) < 1.f ? small.y : big.y};
+  return 0.5f * x * (1.f + erf);
+#else
+  return f32x2{gelu_erf_h(x.x), gelu_erf_h(x.y)};
+#endif
+}
+
 // max over the block of per-thread values v >= 0 (8 waves); one barrier
 __device__ __forceinline__ float block_max8(float v, float* red, int lane, int wave) {
   const float m = wave_max(v);
@@ -55,10 +97,14 @@ __device__ __forceinline__ float block_max8(float v, float* red, int lane, int w
   return fmaxf(fmaxf(fmaxf(r0.x, r0.y), fmaxf(r0.z, r0.w)), fmaxf(fmaxf(r1.x, r1.y), fmaxf(r1.z, r1.w)));
 }
 
-// phase stamp k of this block (wave 0, lane 0) when the debug buffer is set
+// phase stamp k of this block (lane 0 of wave FSMI_MLP_STAMP_WAVE) when the debug buffer is set
+#ifndef FSMI_MLP_STAMP_WAVE
+#define FSMI_MLP_STAMP_WAVE 0
+#endif
 __device__ __forceinline__ void mlp_stamp(const MlpArgs& a, int k) {
-  if (a.ts && threadIdx.x == 0) a.ts[static_cast<size_t>(blockIdx.x) * 8 + k] = wall_clock64();
+  if (a.ts && threadIdx.x == 64 * FSMI_MLP_STAMP_WAVE) a.ts[static_cast<size_t>(blockIdx.x) * 8 + k] = wall_clock64();
 }
+
 
 template <int C>
 __global__ __launch_bounds__(512) void edgenext_mlp_kernel(MlpArgs a) {
@@ -186,10 +232,12 @@ __global__ __launch_bounds__(512) void edgenext_mlp_kernel(MlpArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float2 q = lsb1[hrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hsel];
+      // the two pixel fragments' elements share the row's coefficients: one packed GELU
+      const f32x2 v = fma2(f32x2{acc1[i][0][r], acc1[i][1][r]}, q.x * xinv, q.y);
+      const f32x2 h = gelu_erf_h2(v);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float h = gelu_erf_h(acc1[i][j][r] * (q.x * xinv) + q.y);
-        acc1[i][j][r] = (p0 + j * 32 + rl < HW) ? h : 0.f;     // tail pixels: no effect on the max
+        acc1[i][j][r] = (p0 + j * 32 + rl < HW) ? h[j] : 0.f;     // tail pixels: no effect on the max
         hm = fmaxf(hm, fabsf(acc1[i][j][r]));
       }
     }

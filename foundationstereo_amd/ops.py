@@ -709,6 +709,37 @@ def edgenext_mlp(x: Tensor, res: Tensor, pk1: "PackedConv", bias1: Tensor, pk2: 
     return out
 
 
+def gru_small(hx: Tensor, xc: Tensor, h: Tensor, att: Tensor, pk_zr: "PackedConv", bias_zr: Tensor,
+              pk_q: "PackedConv", bias_q: Tensor, out: Tensor = None) -> Tensor:
+    """SelectiveConvGRU's small (1x1) RaftConvGRU branch weighted by ``att`` in one kernel
+    (core/update.py:83-95,117): ``((1 - z) h + z tanh(convq([r*h, xc]))) * att`` with
+    ``z, r = sigmoid(convz(hx)), sigmoid(convr(hx))``.  ``pk_zr``: PackedConv of [convz; convr]
+    (2Hd x K, 1x1); ``pk_q``: convq's (Hd x K, input channels [r*h, xc])."""
+    _check("gru_small", hx, xc, h, att, bias_zr, bias_q)
+    B, K, H, W = hx.shape
+    Hd = h.shape[1]
+    assert tuple(xc.shape) == (B, K - Hd, H, W) and tuple(h.shape) == (B, Hd, H, W) and \
+        tuple(att.shape) == (B, 1, H, W), \
+        f"gru_small: hx {tuple(hx.shape)}, xc {tuple(xc.shape)}, h {tuple(h.shape)}, att {tuple(att.shape)}"
+    assert pk_zr.k == 1 and pk_q.k == 1 and pk_zr.cin == K and pk_zr.cout == 2 * Hd and pk_q.cin == K and \
+        pk_q.cout == Hd, f"gru_small: zr {pk_zr.cout}x{pk_zr.cin}, q {pk_q.cout}x{pk_q.cin} for K={K}, Hd={Hd}"
+    hx, xc, h, att = _c(hx), _c(xc), _c(h), _c(att)
+    if out is None:
+        out = torch.empty_like(h)
+    else:
+        _check("gru_small", out)
+        if tuple(out.shape) != tuple(h.shape) or not out.is_contiguous():
+            raise RuntimeError(f"gru_small: out must be a contiguous {tuple(h.shape)} fp32 tensor")
+        if any(_overlaps(out, t) for t in (hx, xc, h, att)):
+            raise RuntimeError("gru_small: out must not alias an input")
+    _lib.check(_lib.load().fsmi_gru_small(
+        _p(hx), _p(xc), _p(h), _p(att), _p(out), _p(pk_zr.whi), _p(pk_zr.wlo), _p(pk_zr.scale_bias(bias_zr)),
+        _p(pk_q.whi), _p(pk_q.wlo), _p(pk_q.scale_bias(bias_q)), B, K, Hd, H, W, _stream(hx)), "gru_small")
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * K * 3 * Hd * B * H * W
+    return out
+
+
 def pool2x(x: Tensor) -> Tensor:
     """``F.avg_pool2d(x, 3, stride=2, padding=1)`` (count_include_pad: every window / 9)."""
     _check("pool2x", x)

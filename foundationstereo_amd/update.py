@@ -112,6 +112,15 @@ _BRANCH = [1]
 EARLY_INTERP = os.environ.get("FSMI_EARLY_INTERP", "1") != "0"
 # DispHead's EdgeNeXt MLPs as one fused kernel (ops.edgenext_mlp); FSMI_FUSED_MLP=0: the two 1x1 convs
 _FUSED_MLP = os.environ.get("FSMI_FUSED_MLP", "1") != "0"
+# SelectiveConvGRU's small (1x1) branch as one fused kernel (ops.gru_small, opt-in: FSMI_GRU_SMALL=1); default:
+# the zr gate conv + the convq blend conv.  Alone the fused kernel is faster at every level (cfg2: 97 vs
+# 124, 41 vs 52, 27 vs 101 us at 1/4, 1/8, 1/16, tools/gru_small_bench.py), in the step slower (20.53-20.72
+# vs 20.74-21.00 pairs/s, any subset of levels): its 103-136 KB-LDS blocks wait for a drained CU beside the
+# other streams' conv blocks
+_GRU_SMALL = os.environ.get("FSMI_GRU_SMALL", "0") != "0"
+# ... on maps of at most / at least this many pixels per image (0: any)
+_GRU_SMALL_MAXPIX = int(os.environ.get("FSMI_GRU_SMALL_MAXPIX", "0"))
+_GRU_SMALL_MINPIX = int(os.environ.get("FSMI_GRU_SMALL_MINPIX", "0"))
 
 
 def _branch_stream(device):
@@ -340,6 +349,21 @@ class SelectiveConvGRU(nn.Module):
                 pk, b = _packed(gru.convq)
                 return pk, b, z, rh
 
+            sg = self.small_gru
+            fused_small = (_GRU_SMALL and sg.convq.kernel_size == (1, 1) and h.shape[1] == 128
+                           and hx.shape[1] in (384, 512) and xc.shape[1] == hx.shape[1] - 128
+                           and (not _GRU_SMALL_MAXPIX or h.shape[2] * h.shape[3] <= _GRU_SMALL_MAXPIX)
+                           and h.shape[2] * h.shape[3] >= _GRU_SMALL_MINPIX)
+
+            def small():                                 # out = small branch * att
+                if fused_small:
+                    pkzr, bzr = _packed(sg.convz, sg.convr)
+                    pkq, bq = _packed(sg.convq)
+                    ops.gru_small(hx, xc, h, att, pkzr, bzr, pkq, bq, out=out)
+                else:
+                    pk, b, z, rh = branch(sg, "blend_small")
+                    ops.conv2d_gate([rh, xc], pk, b, "blend_small", h=h, z=z, att=att, out=out)
+
             if OVERLAP and _BRANCH[0]:
                 # small (1x1) branch on a side stream beside the large branch's zr conv; the
                 # large blend adds into ``out`` after the small blend has written it
@@ -347,15 +371,14 @@ class SelectiveConvGRU(nn.Module):
                 side = _branch_stream(h.device)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    pk, b, z, rh = branch(self.small_gru, "blend_small")
-                    ops.conv2d_gate([rh, xc], pk, b, "blend_small", h=h, z=z, att=att, out=out)
+                    small()
                 pk, b, z, rh = branch(self.large_gru, "blend_large")
                 main.wait_stream(side)
                 ops.conv2d_gate([rh, xc], pk, b, "blend_large", h=h, z=z, att=att, out=out)
                 return out
-            for gru, mode in ((self.small_gru, "blend_small"), (self.large_gru, "blend_large")):
-                pk, b, z, rh = branch(gru, mode)
-                ops.conv2d_gate([rh, xc], pk, b, mode, h=h, z=z, att=att, out=out)
+            small()
+            pk, b, z, rh = branch(self.large_gru, "blend_large")
+            ops.conv2d_gate([rh, xc], pk, b, "blend_large", h=h, z=z, att=att, out=out)
             return out
         x = torch.cat(x, dim=1) if len(x) > 1 else x[0]
         x = self.conv0(x)

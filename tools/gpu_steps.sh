@@ -2,7 +2,7 @@
 # GPU steps, one parametrised script (output under $GPU_OUT, default gpurun_out/r5).
 #   bash tools/gpu_steps.sh STEP [STEP ...]
 # Steps:
-#   test        pytest -m gpu (per-test timeout, stops at the first failure)
+#   test        pytest -m gpu (per-test timeout, stops at the first failure; TEST_PATHS, TEST_K = a -k expression)
 #   bench       bench.py cfg2 (20 steps) -> bench_cfg2.json
 #   bench3      bench.py cfg3 -> bench_cfg3.json
 #   trace       rocprofv3 --kernel-trace --stats of the cfg2 bench command
@@ -24,7 +24,8 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     test)
-      timeout -k 10 1100 python3 -u -m pytest ${TEST_PATHS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread ${TEST_ARGS:-} \
+      KARGS=(); [ -n "${TEST_K:-}" ] && KARGS=(-k "$TEST_K")
+      timeout -k 10 1100 python3 -u -m pytest ${TEST_PATHS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread ${TEST_ARGS:-} "${KARGS[@]}" \
         > $OUT/test.log 2>&1 || fail test $? $OUT/test.log
       tail -3 $OUT/test.log ;;
     smoke)
