@@ -49,6 +49,8 @@ SIGNATURES = {
     "fsmi_conv2d_up2_halo_x3": [_P, _I, _PP, _PP, _PP, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_edgenext_mlp": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_stream_create_cumask": [_P, _I, _P],
+    "fsmi_stream_destroy": [_P],
     "fsmi_gru_small": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_pool2x": [_P, _P, _I, _I, _I, _I, _P],

@@ -41,6 +41,10 @@ HEAD_FIRST = os.environ.get("FSMI_HEAD_FIRST", "0") != "0"
 # run_pipelined: the motion encoder's disparity branch (convd1, convd2) on the branch stream, beside the
 # lookup and convc1 / convc2 (A/B knob)
 MOTION_FORK = os.environ.get("FSMI_MOTION_FORK", "0") != "0"
+# run_pipelined: the motion path (lookup + encoder) on the main stream -- it is on the iteration's
+# critical chain between head(t-1) and gru04(t), both on main, with nothing beside it on main -- instead
+# of the motion stream (two cross-stream edges per iteration on that chain); A/B knob
+MOTION_ON_MAIN = os.environ.get("FSMI_MOTION_ON_MAIN", "0") != "0"
 
 
 # the disparity head writes disp + delta into the next encoder buffer (A/B knob)
@@ -501,14 +505,18 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         for t in range(iters):
             if not HEAD_INPLACE and t:
                 enc = disp.new_empty(B, nc + 1, H, W)
-            s_mot.wait_stream(main)
             fork = _side_stream(dev, 1) if MOTION_FORK else None
             if fork is not None:
                 fork.wait_stream(main)                   # forked from the origin (capture_fork)
-            with torch.cuda.stream(s_mot):
+            if MOTION_ON_MAIN:
                 self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
+            else:
+                s_mot.wait_stream(main)
+                with torch.cuda.stream(s_mot):
+                    self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
             main.wait_stream(s_gru)                      # gru08(t): enqueued last on s_gru so far
-            main.wait_stream(s_mot)                      # motion(t)
+            if not MOTION_ON_MAIN:
+                main.wait_stream(s_mot)                  # motion(t)
             if t + 1 < iters:
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru16(t+1), beside gru04(t)
@@ -531,7 +539,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 with torch.cuda.stream(s_gru):           # gru08(t+1), beside the next motion path
                     n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
                 _BRANCH[0] = 1
-                main.wait_stream(s_mot)
+                if not MOTION_ON_MAIN:
+                    main.wait_stream(s_mot)
                 continue
             if t + 1 < iters:
                 s_gru.wait_stream(main)                  # gru04(t)
@@ -555,7 +564,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 disp = self.disp_head(n0, res=disp)
             else:
                 disp = disp + self.disp_head(n0).float()
-            main.wait_stream(s_mot)
+            if not MOTION_ON_MAIN or t + 1 == iters:
+                main.wait_stream(s_mot)
             if fork is not None:
                 main.wait_stream(fork)
         main.wait_stream(s_gru)

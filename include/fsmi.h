@@ -289,6 +289,10 @@ int fsmi_edgenext_mlp(const float* x, const float* res, float* out, const void* 
 int fsmi_gru_small(const float* hx, const float* xc, const float* h, const float* att, float* out,
                    const void* wzhi, const void* wzlo, const float* sbz, const void* wqhi, const void* wqlo,
                    const float* sbq, int B, int K, int Hd, int H, int W, void* stream);
+/* fsmi_stream_create_cumask: a HIP stream restricted to the CUs set in mask (nwords 32-bit words,
+ *   hipExtStreamCreateWithCUMask); fsmi_stream_destroy releases it.  Diagnostics (tools/cumask_probe.py). */
+int fsmi_stream_create_cumask(const unsigned* mask, int nwords, void** stream);
+int fsmi_stream_destroy(void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
  *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */

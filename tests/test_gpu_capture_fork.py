@@ -5,7 +5,8 @@ under capture must fail this test, not the runner):
   * default: gru04's small branch and the motion encoder's disparity branch (convd1, convd2) on the
     branch stream (FSMI_PIPE_BRANCH=1, FSMI_MOTION_FORK=1);
   * FSMI_MOTION_FORK=0: the disparity branch back on the motion stream;
-  * everything in order on its stream (FSMI_PIPE_BRANCH=0, FSMI_MOTION_FORK=0).
+  * everything in order on its stream (FSMI_PIPE_BRANCH=0, FSMI_MOTION_FORK=0);
+  * FSMI_MOTION_ON_MAIN=1: the motion path on the main stream (with and without the fork).
 
 Every configuration runs the same kernels on the same inputs, so the eager forward and the replayed
 graph must be bit-identical across all of them.  faulthandler prints the Python stack of a segfault.
@@ -58,14 +59,16 @@ print(json.dumps({"finite": bool(np.isfinite(rep).all()), "mean": float(rep.mean
 
 CONFIGS = {
     "default": {},
-    "no_motion_fork": {"FSMI_MOTION_FORK": "0"},
+    "motion_fork": {"FSMI_MOTION_FORK": "1"},
     "in_order": {"FSMI_PIPE_BRANCH": "0", "FSMI_MOTION_FORK": "0"},
+    "motion_on_main": {"FSMI_MOTION_ON_MAIN": "1"},
+    "motion_on_main_fork": {"FSMI_MOTION_ON_MAIN": "1", "FSMI_MOTION_FORK": "1"},
 }
 
 
 def _run(name, tmp_path):
     env = dict(os.environ, REPO=REPO, OUT=str(tmp_path / name), **CONFIGS[name])
-    for k in ("FSMI_PIPE_BRANCH", "FSMI_MOTION_FORK"):
+    for k in ("FSMI_PIPE_BRANCH", "FSMI_MOTION_FORK", "FSMI_MOTION_ON_MAIN"):
         if k not in CONFIGS[name]:
             env.pop(k, None)
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
