@@ -99,6 +99,18 @@ for r in recs:
 emit("top launch families (summed kernel time, ms): " + json.dumps(
     {k: round(v / 1e5, 2) for k, v in sorted(fam.items(), key=lambda x: -x[1])[:12]}))
 lk = [i for i, r in enumerate(recs) if r["k"] == _lib.KERNELS.index("lookup")]
+if lk:
+    # before the refinement loop: context net, volume build, 3D filtering, geometry pyramids
+    t_l0 = recs[lk[0]]["s"]
+    pre = [r for r in recs if r["s"] < t_l0]
+    fam_pre = {}
+    for r in pre:
+        f = re.sub(r" (ci|co|h|w|ns)\d+", "", r["tag"])
+        fam_pre[f] = fam_pre.get(f, 0) + min(r["e"], t_l0) - r["s"]
+    emit(f"pre-loop: {(t_l0 - t_first) / 1e5:.2f} ms from the first stamped launch to lookup 0, {len(pre)} launches; "
+         f"post-loop: {(t_last - recs[lk[-1]]['e']) / 1e5:.2f} ms after the last lookup")
+    emit("  pre-loop kernel time by family (ms): " + json.dumps(
+        {k: round(v / 1e5, 3) for k, v in sorted(fam_pre.items(), key=lambda x: -x[1])[:16]}))
 if len(lk) > a.iter + 1:
     first, nxt = recs[lk[a.iter]], recs[lk[a.iter + 1]]
     t0, t1 = first["s"], nxt["s"]
