@@ -39,6 +39,7 @@ ap.add_argument("--config", default="cfg2")
 ap.add_argument("--iter", type=int, default=16)
 ap.add_argument("--replays", type=int, default=5)
 ap.add_argument("--out", default="")
+ap.add_argument("--list", default="", help="regex: also list every launch of the step whose tag matches")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 H, W, md, iters, vit, per = bench.CONFIGS[a.config]
@@ -138,6 +139,11 @@ if len(lk) > a.iter + 1:
          f"{(t1 - t0 - ktime) / 100:.0f} us between them (gaps, unstamped kernels)")
     for r in chain:
         emit(f"    {r['stream']:>8} {(r['s'] - t0) / 100:8.1f} {(r['e'] - t0) / 100:8.1f} {(r['e'] - r['s']) / 100:7.1f}  {r['tag']}")
+if a.list:
+    rx = re.compile(a.list)
+    for r in recs:
+        if rx.search(r["tag"]):
+            emit(f"  {r['stream']:>8} {(r['s'] - t_first) / 100:10.1f} {(r['e'] - r['s']) / 100:7.1f}  {r['tag']}")
 if a.out:
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
