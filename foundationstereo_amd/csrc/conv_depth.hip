@@ -211,6 +211,147 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------- (3, 3, 3): cfg 31
+// The same plane walk for the 3^3 convs of corr_stem / the ResNet blocks / the classifier
+// (core/foundation_stereo.py:164-176, core/submodule.py:51-86,159-195).  On the generic volume tile
+// each (output depth, kd) pair stages its own 32-channel chunk, so every input plane is staged three
+// times and feeds 54 MFMAs per wave each time (~15 % of the MFMA rate at cfg2's 28-channel stem).
+// Here a block owns DB = 8 output depths of a 4 x 32 pixel tile (wave w: row w, all 8 depths):
+// staged plane U feeds output j = U - kd, kd in [0, 3), over all 9 spatial taps -- up to 3 outputs
+// x 9 taps x 2 k-steps x 3 products = 162 MFMAs per wave per staging, (DB + 2) / DB stagings per
+// output; the plane walk is unrolled so every accumulator index is a constant.  The (27 taps x 32 x
+// 32) hi / lo weight slab of a chunk sits in LDS for the whole walk (108 KB, swizzled as above),
+// the plane's halo (6 x 34 pixels) beside it: 141 KB, one block per CU.
+constexpr int kD3DB = 8;           // output depths per block
+constexpr int kD3TR = 4;           // pixel rows per block (x 32 columns): wave w owns row w
+
+__global__ __launch_bounds__(256) void conv_depth3_kernel(HaloArgs a) {
+  constexpr int KD = 3, KS = 3, NTAP = KS * KS, DB = kD3DB, TR = kD3TR, NP = DB + KD - 1;
+  using HS = HaloStage<KS, TR>;
+  __shared__ __attribute__((aligned(16))) _Float16 Wh[KD * NTAP][32][32];
+  __shared__ __attribute__((aligned(16))) _Float16 Wl[KD * NTAP][32][32];
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[HS::NHP][HROW];
+  __shared__ __attribute__((aligned(16))) float red[4];
+
+  const int tid = threadIdx.x, lane = tid & 63, row = tid >> 6;
+  const int hsel = lane >> 5, rl = lane & 31;
+
+  // block -> (cout tile, b, row tile, col tile, depth tile), depth fastest
+  const unsigned item = xcd_remap(blockIdx.x, gridDim.x);
+  const int ndt = (a.D + DB - 1) / DB;
+  int rest = static_cast<int>(item);
+  const int dt = rest % ndt; rest /= ndt;
+  const int ct = rest % a.nct; rest /= a.nct;
+  const int rt = rest % a.nrt; rest /= a.nrt;
+  const int b = rest % a.B;
+  const int m0 = (rest / a.B) * 32;
+  const int d0 = dt * DB, r0 = rt * TR, c0 = ct * 32;
+  const int nck = a.CinP / HKC;
+  __shared__ EpiCoef<32> ecoef;                    // visible to the epilogue after the plane barriers
+  ecoef.fill(a, m0, tid, 256);
+
+  HS hs, hs2;
+  hs.init(a, tid, r0, c0);
+  hs2.init(a, tid, r0, c0);
+  f32x16 acc[DB];
+#pragma unroll
+  for (int j = 0; j < DB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  int sx = kNoExp, smin = kNoExp;
+  bool ovf = false;
+  for (int cc = 0; cc < nck; ++cc) {
+    __syncthreads();               // the previous chunk's weights and plane are no longer read
+    // weight slab of chunk cc: [(kd, kh, kw)][cout m0..m0+31][32 cin] (the packing's tap order)
+    for (int e = tid; e < KD * NTAP * 32 * 4; e += 256) {
+      const int s4 = e & 3, m = (e >> 2) & 31, kt = e >> 7;
+      const size_t off = (static_cast<size_t>(kt * nck + cc) * a.CoutP + min(m0 + m, a.CoutP - 1)) * HKC + 8 * s4;
+      const uint4 h = *reinterpret_cast<const uint4*>(a.whi + off);
+      const uint4 l = *reinterpret_cast<const uint4*>(a.wlo + off);
+      *reinterpret_cast<uint4*>(&Wh[kt][m][8 * wslot(m, s4)]) = h;
+      *reinterpret_cast<uint4*>(&Wl[kt][m][8 * wslot(m, s4)]) = l;
+    }
+    // planes d0 - 1 .. d0 + DB, walked in order (zeros outside [0, D): HaloStage::load)
+    hs.load(a, b, cc, d0 - 1);
+    hs2.load(a, b, cc, d0);
+    static_for<0, NP>([&](auto u_c) FSMI_HALO_INL {
+      constexpr int U = decltype(u_c)::value;
+      HS& st = (U & 1) ? hs2 : hs;
+      const float m = wave_max(st.absmax());
+      if (lane == 0) red[row] = m;
+      __syncthreads();             // every wave is done with the previous plane; maxima visible
+      const float bm = red4_max(red);
+      ovf |= !(bm <= 3.4e38f);
+      // per-plane exponent, both directions, as conv_depth_kernel
+      const int fit = __builtin_amdgcn_readfirstlane(chunk_exp(bm));
+      if (fit != kNoExp && (fit < sx || (sx != kNoExp && fit > sx + 8))) {
+        int se = __builtin_amdgcn_readfirstlane(chunk_exp<kHeadroom1>(bm));
+        if (sx != kNoExp) {
+          se = min(se, smin + 60);
+          const float f = exp2i(se - sx);
+#pragma unroll
+          for (int j = 0; j < DB; ++j) acc[j] *= f;
+        }
+        sx = se;
+        smin = min(smin, se);
+      }
+      st.template store<1>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
+      if constexpr (U + 2 < NP) st.load(a, b, cc, d0 - 1 + U + 2);   // in flight during the next two planes
+      __syncthreads();
+      // plane U feeds outputs j = U - kd in [0, DB): compile-time indices throughout
+#pragma unroll
+      for (int tap = 0; tap < NTAP; ++tap) {
+        const int hp = (row + tap / KS) * HS::HC + rl + tap % KS;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const half8 bh = *reinterpret_cast<const half8*>(&Xh[hp][16 * k + 8 * hsel]);
+          const half8 bl = *reinterpret_cast<const half8*>(&Xl[hp][16 * k + 8 * hsel]);
+          const int sl = wslot(rl, 2 * k + hsel);
+          static_for<0, KD>([&](auto kd_c) FSMI_HALO_INL {
+            constexpr int KDI = decltype(kd_c)::value, J = U - KDI;
+            if constexpr (J >= 0 && J < DB) {
+              const half8 ah = *reinterpret_cast<const half8*>(&Wh[KDI * NTAP + tap][rl][8 * sl]);
+              const half8 al = *reinterpret_cast<const half8*>(&Wl[KDI * NTAP + tap][rl][8 * sl]);
+              if constexpr (FSMI_NPROD == 3) {
+                acc[J] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[J], 0, 0, 0);
+                acc[J] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[J], 0, 0, 0);
+              }
+              acc[J] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[J], 0, 0, 0);
+            }
+          });
+        }
+      }
+    });
+  }
+  flag_overflow(a, ovf);
+  const float xinv = exp2i(sx == kNoExp ? 0 : -sx);
+  const int hh = r0 + row, ww = c0 + rl;
+  if (hh >= a.H || ww >= a.W) return;
+  const long long P = static_cast<long long>(a.H) * a.W;
+  const int hw2 = hh * a.W + ww;
+  const int cb = m0 + 4 * hsel;
+  auto epi = [&](auto act_c) FSMI_HALO_INL {
+    constexpr int ACT = decltype(act_c)::value;
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      const int d = d0 + j;
+      if (d >= a.D) break;
+      const long long hw = static_cast<long long>(d) * P + hw2;
+      FragCoef cf;
+      frag_coef_lds<ACT>(xinv, 4 * hsel, ecoef.sb, ecoef.g, cf);
+      store_frag_c<ACT, true>(a, acc[j], cf, cb, b, hw, hw2, a.out, a.res, a.gh, a.gz, a.gatt, a.grh);
+    }
+  };
+  switch (a.act) {
+    case 1: epi(std::integral_constant<int, 1>()); break;
+    case 6: epi(std::integral_constant<int, 6>()); break;
+    default: epi(std::integral_constant<int, 0>()); break;
+  }
+}
+
 }  // namespace
 
 namespace halo {
@@ -232,6 +373,23 @@ int launch_depth(HaloArgs& a, hipStream_t s) {
   // scratch (56-64 B) -- it runs in the 3D filter only, outside the refinement loop's timeline
   a.clk = nullptr;
   hipLaunchKernelGGL((conv_depth_kernel<17>), dim3(static_cast<unsigned>(grid)), dim3(256), 0, s, a);
+  return FSMI_OK;
+}
+
+bool depth3_conv_ok(const HaloArgs& a) { return a.KD == 3 && a.str == 1 && !a.up && a.D > 1; }
+
+// (3, 3, 3) stride-1 volume conv on the depth-blocked 3^3 tile (cfg 31), fields as launch_depth
+int launch_depth3(HaloArgs& a, hipStream_t s) {
+  if (!depth3_conv_ok(a)) {
+    set_error("fsmi_conv3d_halo: tile 31 takes (3, 3, 3) stride-1 volume convs");
+    return FSMI_ERR_ARG;
+  }
+  a.nrt = (a.H + kD3TR - 1) / kD3TR;
+  a.nct = (a.W + 31) / 32;
+  const long long ndt = (a.D + kD3DB - 1) / kD3DB;
+  const long long grid = static_cast<long long>(a.CoutP / 32) * a.B * a.nrt * a.nct * ndt;
+  a.clk = nullptr;
+  hipLaunchKernelGGL(conv_depth3_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, s, a);
   return FSMI_OK;
 }
 
