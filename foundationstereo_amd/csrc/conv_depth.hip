@@ -222,7 +222,10 @@ __global__ __launch_bounds__(256) void conv_depth_kernel(HaloArgs a) {
 // x 9 taps x 2 k-steps x 3 products = 162 MFMAs per wave per staging, (DB + 2) / DB stagings per
 // output; the plane walk is unrolled so every accumulator index is a constant.  The (27 taps x 32 x
 // 32) hi / lo weight slab of a chunk sits in LDS for the whole walk (108 KB, swizzled as above),
-// the plane's halo (6 x 34 pixels) beside it: 141 KB, one block per CU.
+// the plane's halo (6 x 34 pixels) beside it: 141 KB, one block per CU.  Measured (cfg2 stem, 28 ->
+// 28 at 48 x 120 x 160): 471 us vs 373 on the generic tile -- the compiler issues each A / B read
+// right before its MFMAs with a full lgkmcnt wait (only 16 VGPRs left for operands at the 256-VGPR
+// limit), so the tile stays opt-in (explicit cfg 31).
 constexpr int kD3DB = 8;           // output depths per block
 constexpr int kD3TR = 4;           // pixel rows per block (x 32 columns): wave w owns row w
 
@@ -252,9 +255,8 @@ __global__ __launch_bounds__(256) void conv_depth3_kernel(HaloArgs a) {
   __shared__ EpiCoef<32> ecoef;                    // visible to the epilogue after the plane barriers
   ecoef.fill(a, m0, tid, 256);
 
-  HS hs, hs2;
-  hs.init(a, tid, r0, c0);
-  hs2.init(a, tid, r0, c0);
+  HS hs;                           // one register set, loaded one plane ahead (two sets took the
+  hs.init(a, tid, r0, c0);         // VGPRs the MFMA operands need to be read ahead)
   f32x16 acc[DB];
 #pragma unroll
   for (int j = 0; j < DB; ++j)
@@ -276,10 +278,9 @@ __global__ __launch_bounds__(256) void conv_depth3_kernel(HaloArgs a) {
     }
     // planes d0 - 1 .. d0 + DB, walked in order (zeros outside [0, D): HaloStage::load)
     hs.load(a, b, cc, d0 - 1);
-    hs2.load(a, b, cc, d0);
     static_for<0, NP>([&](auto u_c) FSMI_HALO_INL {
       constexpr int U = decltype(u_c)::value;
-      HS& st = (U & 1) ? hs2 : hs;
+      HS& st = hs;
       const float m = wave_max(st.absmax());
       if (lane == 0) red[row] = m;
       __syncthreads();             // every wave is done with the previous plane; maxima visible
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(256) void conv_depth3_kernel(HaloArgs a) {
         smin = min(smin, se);
       }
       st.template store<1>(Xh, Xl, tid, exp2i(sx == kNoExp ? 0 : sx), ovf);
-      if constexpr (U + 2 < NP) st.load(a, b, cc, d0 - 1 + U + 2);   // in flight during the next two planes
+      if constexpr (U + 1 < NP) st.load(a, b, cc, d0 - 1 + U + 1);   // in flight during this plane's MFMAs
       __syncthreads();
       // plane U feeds outputs j = U - kd in [0, DB): compile-time indices throughout
 #pragma unroll
