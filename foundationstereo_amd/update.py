@@ -93,8 +93,8 @@ def _side_stream(device, idx=0):
     gru16 / gru08 pipeline of ``run_pipelined``)."""
     s = _SIDE.get((device, idx))
     if s is None:
-        # all at default priority: the motion stream at high priority (its lookup dispatched ahead
-        # of the pipeline stream's conv blocks) measured 14.7 vs 19.0 pairs/s (round 4)
+        # all at default priority: ANY side stream at high priority -- motion (round 4), the branch or
+        # the pipeline stream (round 5) -- measured 14.5-14.7 vs 19.0-20.9 pairs/s
         s = _SIDE[(device, idx)] = torch.cuda.Stream(device=device)
     return s
 
