@@ -503,12 +503,16 @@ struct SegBases {
 // group); per task a packed descriptor (clamped pixel offset << 3 | in-image << 2
 // | group) computed once per block; a chunk is loaded into registers one chunk
 // ahead and split into fp16 hi/lo when stored to LDS.
-template <int KS, int TR, int STR = 1>
+// DEFER: keep the raw loads and mask them where they are read (absmax / store), so the loads stay in
+// flight until then; otherwise they are masked on arrival -- which the compiler schedules right after
+// the loads, waiting on them there (the default, kept for the tuned tiles' register budgets).
+template <int KS, int TR, int STR = 1, bool DEFER = false>
 struct HaloStage {
   // STR = 2: a stride-2 conv's window, (2 TR + 1) x 65 input pixels for TR x 32 outputs
   static constexpr int PD = KS / 2, HR = STR * (TR - 1) + KS, HC = STR * 31 + KS, NHP = HR * HC;
   static constexpr int X_TASKS = NHP * (HKC / 8), X_PER_T = (X_TASKS + 255) / 256;
   int desc[X_PER_T];
+  int lim[DEFER ? X_PER_T : 1];    // DEFER: channels of task u's group that hold data (0 outside)
   f32x8 xv[X_PER_T];
 
   __device__ __forceinline__ void init(const HaloArgs& a, int tid, int r0, int c0) {
@@ -544,20 +548,33 @@ struct HaloStage {
       // over constant indices, so the kernarg arrays are never indexed per lane
       const gcfptr src = seg.chan(a, cic, HW) + poff + pix;
       const bool ok = (desc[u] & 4) && plane_ok;
-      f32x8 v;
-      if (full) {
+      if constexpr (DEFER) {
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = src[static_cast<size_t>(j) * HW];
-      } else {
-        const int nv = a.Cin - ci0;                // may be <= 0 in the padded tail
+          for (int j = 0; j < 8; ++j) xv[u][j] = src[static_cast<size_t>(j) * HW];
+          lim[u] = ok ? 8 : 0;
+        } else {
+          const int nv = a.Cin - ci0;              // may be <= 0 in the padded tail
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float t = src[static_cast<size_t>(max(0, min(j, nv - 1))) * HW];
-          v[j] = j < nv ? t : 0.f;
+          for (int j = 0; j < 8; ++j) xv[u][j] = src[static_cast<size_t>(max(0, min(j, nv - 1))) * HW];
+          lim[u] = ok ? max(0, min(nv, 8)) : 0;
         }
-      }
+      } else {
+        f32x8 v;
+        if (full) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[u][j] = ok ? v[j] : 0.f;
+          for (int j = 0; j < 8; ++j) v[j] = src[static_cast<size_t>(j) * HW];
+        } else {
+          const int nv = a.Cin - ci0;              // may be <= 0 in the padded tail
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float t = src[static_cast<size_t>(max(0, min(j, nv - 1))) * HW];
+            v[j] = j < nv ? t : 0.f;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[u][j] = ok ? v[j] : 0.f;
+      }
     }
   }
 
@@ -568,7 +585,7 @@ struct HaloStage {
 #pragma unroll
     for (int u = 0; u < X_PER_T; ++u)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(xv[u][j]));
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, !DEFER || j < lim[DEFER ? u : 0] ? fabsf(xv[u][j]) : 0.f);
     return m;
   }
 
@@ -582,7 +599,9 @@ struct HaloStage {
       const int task = tid + 256 * u;
       if (X_TASKS % 256 == 0 || task < X_TASKS) {
         const int hp = task % NHP, g = task / NHP;
-        const f32x8 x = xv[u] * scale;
+        f32x8 x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = !DEFER || j < lim[DEFER ? u : 0] ? xv[u][j] * scale : 0.f;
         if constexpr (RMODE == 2) {               // largest scaled |x| of the task, one compare after
           float m = 0.f;
 #pragma unroll

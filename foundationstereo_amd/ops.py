@@ -410,7 +410,10 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
         _CONV_FLOPS["flops"] += 2 * Cin * pk.cout * pk.kd * pk.k * pk.k * B * Do * Ho * Wo
     stream = _stream(x)
     ws = _split_workspace(x.device, stream, 8 * B * pk.cout * Do * Ho * Wo)
+    auto = cfg < 0
     cfg, nsplit = _tuned(pk.k if stride == 1 else f"{pk.k}s2", pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
+    if auto and _DEPTH3_TILE and stride == 1 and pk.k == 3 and pk.kd == 3 and Cin <= 32 and D > 1:
+        cfg, nsplit = 31, 1            # the rolled depth-blocked 3^3 walk (one 32-channel chunk)
     if cfg == 30 and not _DEPTH_TILE:
         cfg, nsplit = -1, -1           # A/B: the generic volume tiles (the C side picks)
     _lib.check(_lib.load().fsmi_conv3d_halo_x3_ex(
@@ -609,6 +612,9 @@ _SPLIT_CAP = int(os.environ.get("FSMI_SPLIT_CAP", "2"))
 # (17, 1, 1) volume convs (Conv3dNormActReduced.conv2) on the depth-blocked tile (cfg 30); 0: the
 # generic volume tiles from the tuning table (A/B)
 _DEPTH_TILE = os.environ.get("FSMI_DEPTH_TILE", "1") != "0"
+# (3, 3, 3) stride-1 volume convs of at most 32 input channels (corr_stem, the classifier) on the
+# rolled depth-blocked 3^3 tile (cfg 31) instead of the table's generic volume tile; 0: the table
+_DEPTH3_TILE = os.environ.get("FSMI_DEPTH3_TILE", "0") != "0"
 
 
 _SPLIT_WS = {}

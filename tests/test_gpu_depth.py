@@ -158,3 +158,18 @@ def test_depth3_conv_feature_gate(ops_mod):
     ref = F.leaky_relu(F.conv3d(x.double(), w.double(), bias.double(), padding=1), 0.01) * \
         torch.sigmoid(fatt.double())[:, :, None]
     close(out, ref)
+
+
+def test_depth3_auto_knob(ops_mod, monkeypatch):
+    """FSMI_DEPTH3_TILE: auto-chosen (3, 3, 3) stride-1 convs of <= 32 input channels run the rolled
+    3^3 walk (cfg 31); wider inputs keep the table's tile."""
+    monkeypatch.setattr(ops_mod, "_DEPTH3_TILE", True)
+    gen = torch.Generator().manual_seed(93)
+    for cin, want in ((28, 1), (40, 0)):
+        x = torch.randn(1, cin, 13, 6, 40, generator=gen)
+        w = torch.randn(28, cin, 3, 3, 3, generator=gen) * 0.08
+        pk = ops_mod.PackedConv(g(w), mode="halo")
+        before = ops_mod.conv_launch_counts()[31]
+        out = ops_mod.conv3d(g(x), pk, act="leaky")
+        assert ops_mod.conv_launch_counts()[31] - before == want
+        close(out, F.leaky_relu(F.conv3d(x.double(), w.double(), padding=1), 0.01))

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The (3, 3, 3) volume convs of the 3D filter at cfg2 (and cfg5's full-resolution stem) on the
 depth-blocked tile (cfg 31) vs the tuning table's choice, each the mean over a replayed graph of
-10 launches, with the max |diff| between the two.  GPU box: python tools/depth3_bench.py"""
+10 launches, with the max |diff| between the two.  GPU box: python tools/depth3_bench.py [--only NAME]"""
 import json
 import os
 import sys
@@ -36,8 +36,11 @@ def timed(fn, reps=10):
 SHAPES = [(28, 28, 48, 120, 160, "leaky", "stem 3^3"), (28, 14, 48, 120, 160, "leaky", "classifier 28->14"),
           (14, 14, 48, 120, 160, "leaky", "classifier 14->14"), (56, 56, 24, 60, 80, "leaky", "hourglass 56"),
           (28, 28, 80, 256, 384, "leaky", "cfg5 full-res stem")]
+ONLY = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None   # layer-name prefix
 with torch.no_grad():
     for cin, cout, D, H, W, act, name in SHAPES:
+        if ONLY and not name.startswith(ONLY):
+            continue
         x = torch.randn(1, cin, D, H, W, device=dev)
         pk = ops.PackedConv(torch.randn(cout, cin, 3, 3, 3, device=dev) * 0.05, mode="halo")
         b = torch.randn(cout, device=dev)
