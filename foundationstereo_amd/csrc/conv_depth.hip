@@ -528,7 +528,8 @@ int launch_depth3(HaloArgs& a, hipStream_t s) {
   }
   a.nrt = (a.H + kD3TR - 1) / kD3TR;
   a.nct = (a.W + 31) / 32;
-  const bool rolled = a.CinP == HKC;              // one chunk: the rolled ring walk
+  // one chunk, one input segment, byte offsets of a batch item in 32 bits: the rolled ring walk
+  const bool rolled = a.CinP == HKC && a.nseg == 1 && static_cast<long long>(a.Cin) * a.cstride * 4 < (1LL << 32);
   const int db = rolled ? kD3RDB : kD3DB;
   const long long ndt = (a.D + db - 1) / db;
   const long long grid = static_cast<long long>(a.CoutP / 32) * a.B * a.nrt * a.nct * ndt;

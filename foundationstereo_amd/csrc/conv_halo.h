@@ -549,16 +549,24 @@ struct HaloStage {
       const gcfptr src = seg.chan(a, cic, HW) + poff + pix;
       const bool ok = (desc[u] & 4) && plane_ok;
       if constexpr (DEFER) {
-        if (full) {
+        // one input segment of < 4 GB per batch item (the launcher checks): byte offsets from the
+        // block-uniform base, channel j of the group at ob0 + j * HW * 4, clamped to the group's last
+        // channel with one min (offsets grow with j) -- two VALU per load instead of a 64-bit product
+        const int nv = a.Cin - ci0;                // may be <= 0 in the padded tail
+        const int last = max(0, min(nv, 8) - 1);
+        const unsigned hwb = static_cast<unsigned>(HW) * 4u;
+        const unsigned ob0 = (static_cast<unsigned>(cic) * static_cast<unsigned>(HW) +
+                              static_cast<unsigned>(poff) + static_cast<unsigned>(pix)) * 4u;
+        const unsigned oblast = ob0 + static_cast<unsigned>(last) * hwb;
+        using gccptr = const __attribute__((address_space(1))) char*;
+        const gccptr base = reinterpret_cast<gccptr>(seg.p[0]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) xv[u][j] = src[static_cast<size_t>(j) * HW];
-          lim[u] = ok ? 8 : 0;
-        } else {
-          const int nv = a.Cin - ci0;              // may be <= 0 in the padded tail
-#pragma unroll
-          for (int j = 0; j < 8; ++j) xv[u][j] = src[static_cast<size_t>(max(0, min(j, nv - 1))) * HW];
-          lim[u] = ok ? max(0, min(nv, 8)) : 0;
+        for (int j = 0; j < 8; ++j) {
+          const unsigned ob = full ? ob0 + j * hwb : min(ob0 + j * hwb, oblast);
+          xv[u][j] = *reinterpret_cast<gcfptr>(base + ob);
         }
+        lim[u] = ok ? (full ? 8 : max(0, min(nv, 8))) : 0;
+        (void)src;
       } else {
         f32x8 v;
         if (full) {
