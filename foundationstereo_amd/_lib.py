@@ -48,6 +48,16 @@ SIGNATURES = {
     "fsmi_conv3d_up2_halo_x3": [_P, _I, _PP, _PP, _PP, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_conv2d_up2_halo_x3": [_P, _I, _PP, _PP, _PP, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_dwconv2d_ex": [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_channel_layernorm": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
+    "fsmi_vit_attention": [_P, _P, _I, _I, _I, _I, _I, _F, _P],
+    "fsmi_space_to_depth": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_depth_to_space": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "fsmi_vit_tokens": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "fsmi_resize_bicubic": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "fsmi_instance_norm": [_P, _P, _P, _I, _I, _F, _I, _I, _P],
+    "fsmi_elementwise": [_P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _I, _P],
+    "fsmi_xca": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_edgenext_mlp": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_stream_create_cumask": [_P, _I, _P],
     "fsmi_stream_destroy": [_P],

@@ -32,18 +32,21 @@ def load_cfg(ckpt_path: str, overrides: Optional[dict] = None) -> StereoArgs:
 
 
 def load_model(ckpt_path: str, overrides: Optional[dict] = None, device=None,
-               feature=None) -> Tuple[torch.nn.Module, dict]:
+               feature=None, backbone: bool = False) -> Tuple[torch.nn.Module, dict]:
     """FoundationStereo with the checkpoint's ``model`` state loaded strictly, in eval mode
     (scripts/run_demo.py:121-129).  Returns (model, meta): meta holds the checkpoint's
     ``global_step`` / ``epoch`` and ``skipped_backbone_keys``.
 
-    A real checkpoint carries the backbone's ``feature.*`` weights (EdgeNeXt + DepthAnythingV2,
-    out of this package's scope).  When ``feature`` is None (the parameter-free synthetic
+    A real checkpoint carries the backbone's ``feature.*`` weights (EdgeNeXt + DepthAnythingV2).  When ``feature`` is None (the parameter-free synthetic
     stand-in) or has no parameters of its own, those keys cannot be loaded anywhere: they are
     set aside and listed in ``meta["skipped_backbone_keys"]``, and every other key still loads
-    strictly.  With a backbone that has parameters, ``feature.*`` must match it exactly."""
+    strictly.  With a backbone that has parameters (``backbone=True``: the real ``Feature``,
+    core/extractor.py:323-369), ``feature.*`` must match it exactly."""
     from .foundation_stereo import FoundationStereo
     args = load_cfg(ckpt_path, overrides)
+    if backbone and feature is None:
+        from .backbone import Feature
+        feature = Feature(args)
     model = FoundationStereo(args, feature=feature)
     ckpt = torch.load(ckpt_path, map_location="cpu", weights_only=True)
     if not isinstance(ckpt, dict) or "model" not in ckpt:

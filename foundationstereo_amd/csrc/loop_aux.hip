@@ -1,5 +1,6 @@
 // Refinement-loop auxiliaries that MIOpen / ATen run poorly at these shapes:
-//  * depthwise KxK conv (EdgeNeXt dwconv of DispHead, core/submodule.py:565-591):
+//  * depthwise KxK conv (EdgeNeXt dwconv of DispHead, core/submodule.py:565-591, and of the backbone's
+//    EdgeNeXt-S ConvBlocks / SplitTransposeBlocks, core/extractor.py:327):
 //    MIOpen routes it through NCHW->NHWC transposes and a grouped CK kernel
 //    (~105 us at 128x120x160); here it is one LDS-tiled pass (HBM-bound: one
 //    read + one write of the plane);
@@ -14,23 +15,29 @@ constexpr int DW_TR = 16, DW_TC = 64;   // conv_1in output tile per block (rows 
 // outputs and each LDS window row feeds up to 8 accumulators (16 x 64 with 4 rows: 1 TB/s at cfg2)
 constexpr int DWK_TR = 32, DWK_RPT = 8;
 
+// x / add / out planes (b, c) at (b * ctot + c) * H * W of their tensors (channel slices of wider maps);
+// add (optional) is summed into the input as it is staged (EdgeNeXt's multi-scale split, the
+// `sp = sp + spx[i]` before each depthwise conv, timm edgenext SplitTransposeBlock)
 template <int KS>
-__global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ add,
+                                                     const float* __restrict__ w,
                                                      const float* __restrict__ bias, float* __restrict__ out,
-                                                     int C, int H, int W, int ntr, int ntc,
-                                                     unsigned long long* clk) {
+                                                     int C, int H, int W, int ntr, int ntc, int xct, int adct,
+                                                     int oct, unsigned long long* clk) {
   FSMI_TIMELINE_CLOCK(clk);
   constexpr int P = KS / 2, IR = DWK_TR + KS - 1, IC = DW_TC + KS - 1, RPT = DWK_RPT;
   __shared__ float tile[IR][IC + 1];
   const int plane = blockIdx.x / (ntr * ntc);
   const int t = blockIdx.x - plane * ntr * ntc;
   const int r0 = (t / ntc) * DWK_TR, c0 = (t % ntc) * DW_TC;
-  const int c = plane % C;
-  const float* xp = x + static_cast<size_t>(plane) * H * W;
+  const int c = plane % C, bimg = plane / C;
+  const float* xp = x + (static_cast<size_t>(bimg) * xct + c) * H * W;
+  const float* ap = add ? add + (static_cast<size_t>(bimg) * adct + c) * H * W : nullptr;
   for (int e = threadIdx.x; e < IR * IC; e += 256) {
     const int ir = e / IC, ic = e - ir * IC;
     const int hh = r0 + ir - P, ww = c0 + ic - P;
-    tile[ir][ic] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xp[hh * W + ww] : 0.f;
+    const bool in = hh >= 0 && hh < H && ww >= 0 && ww < W;
+    tile[ir][ic] = in ? xp[hh * W + ww] + (ap ? ap[hh * W + ww] : 0.f) : 0.f;
   }
   float wk[KS * KS];
 #pragma unroll
@@ -55,7 +62,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
       }
     }
   }
-  float* op = out + static_cast<size_t>(plane) * H * W;
+  float* op = out + (static_cast<size_t>(bimg) * oct + c) * H * W;
 #pragma unroll
   for (int o = 0; o < RPT; ++o) {
     const int hh = r0 + rb + o, ww = c0 + col;
@@ -169,20 +176,32 @@ __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x
 
 using namespace fsmi;
 
-extern "C" int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
-                             int H, int W, void* stream) {
+extern "C" int fsmi_dwconv2d_ex(const float* x, int x_ctot, const float* add, int add_ctot, const float* w,
+                                const float* bias, float* out, int out_ctot, int B, int C, int KS, int H, int W,
+                                void* stream) {
   FSMI_CHECK_ARG(x && w && out, "fsmi_dwconv2d: null pointer");
   FSMI_CHECK_ARG(B > 0 && C > 0 && H > 0 && W > 0, "fsmi_dwconv2d: bad shape");
-  FSMI_CHECK_ARG(KS == 3 || KS == 5 || KS == 7, "fsmi_dwconv2d: kernel %d unsupported (3, 5, 7)", KS);
+  FSMI_CHECK_ARG(x_ctot >= C && out_ctot >= C && (!add || add_ctot >= C), "fsmi_dwconv2d: channel slice wider than "
+                 "its tensor");
+  FSMI_CHECK_ARG(KS == 3 || KS == 5 || KS == 7 || KS == 9, "fsmi_dwconv2d: kernel %d unsupported (3, 5, 7, 9)", KS);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_DWCONV, s);
   const int ntr = (H + DWK_TR - 1) / DWK_TR, ntc = (W + DW_TC - 1) / DW_TC;
   const dim3 grid(static_cast<unsigned>(B) * C * ntr * ntc);
   unsigned long long* clk = clock_slot(FSMI_K_DWCONV, s, 4ll * grid.x * grid.y * grid.z, "dwconv", true);
-  if (KS == 7) hipLaunchKernelGGL(dwconv_kernel<7>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc, clk);
-  else if (KS == 5) hipLaunchKernelGGL(dwconv_kernel<5>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc, clk);
-  else hipLaunchKernelGGL(dwconv_kernel<3>, grid, dim3(256), 0, s, x, w, bias, out, C, H, W, ntr, ntc, clk);
+#define FSMI_DW_LAUNCH(K) hipLaunchKernelGGL(dwconv_kernel<K>, grid, dim3(256), 0, s, x, add, w, bias, out, C, H, W, \
+                                             ntr, ntc, x_ctot, add_ctot, out_ctot, clk)
+  if (KS == 7) FSMI_DW_LAUNCH(7);
+  else if (KS == 5) FSMI_DW_LAUNCH(5);
+  else if (KS == 9) FSMI_DW_LAUNCH(9);
+  else FSMI_DW_LAUNCH(3);
+#undef FSMI_DW_LAUNCH
   return finish_launch("fsmi_dwconv2d");
+}
+
+extern "C" int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out, int B, int C, int KS,
+                             int H, int W, void* stream) {
+  return fsmi_dwconv2d_ex(x, C, nullptr, C, w, bias, out, C, B, C, KS, H, W, stream);
 }
 
 extern "C" int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,

@@ -13,8 +13,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import synth
-from .submodule import BasicConv, _fast2d, _fast_s2_2d, conv2d_bn_act, conv2d_s2_bn_act
+from . import ops, synth
+from .submodule import BasicConv, _fast2d, _fast_s2_2d, _hip_in, conv2d_bn_act, conv2d_s2_bn_act
 
 __all__ = ["ResidualBlock", "ContextNetDino", "DepthAnythingFeature", "SyntheticFeature"]
 
@@ -74,6 +74,13 @@ class ResidualBlock(nn.Module):
                     return conv2d_s2_bn_act(x, pc, n3, "relu", res=y, res_pre=True)
                 x = self.downsample(x)
             return torch.relu_(y.add_(x))
+        if (self.downsample is None and _hip_in(self.norm1, x) and _hip_in(self.norm2, x)
+                and _fast2d(x, self.conv1, None) and _fast2d(x, self.conv2, None)):
+            # norm_fn='instance' (Feature.conv4): relu(x + relu(IN(conv2(relu(IN(conv1 x))))))
+            x = x.float()
+            y = ops.instance_norm(conv2d_bn_act([x], self.conv1, None), act="relu", eps=self.norm1.eps)
+            return ops.instance_norm(conv2d_bn_act([y], self.conv2, None), act="relu", res=x, act2="relu",
+                                     eps=self.norm2.eps)
         y = F.relu(self.norm1(self.conv1(x)))
         y = F.relu(self.norm2(self.conv2(y)))
         if self.downsample is not None:

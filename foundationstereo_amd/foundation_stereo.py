@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from . import ops
 from . import submodule as _sub
 from . import update as _update
+from .backbone import Feature
 from .extractor import ContextNetDino, SyntheticFeature
 from .geometry import Combined_Geo_Encoding_Volume
 from .submodule import (BasicConv, BasicConv_IN, ChannelAttentionEnhancement, Conv2x, Conv3dNormActReduced,
@@ -211,7 +212,8 @@ def _poison_outputs(out):
 
 
 class FoundationStereo(nn.Module):
-    """core/foundation_stereo.py:127-274 (minus the out-of-scope backbone)."""
+    """core/foundation_stereo.py:127-274.  ``feature``: the backbone module (default: ``Feature`` when
+    ``args.backbone == "real"``, else the synthetic stand-in whose features are preset in HBM)."""
 
     def __init__(self, args, feature=None):
         super().__init__()
@@ -225,7 +227,12 @@ class FoundationStereo(nn.Module):
         self.cam = ChannelAttentionEnhancement(self.args.hidden_dims[0])
         self.context_zqr_convs = nn.ModuleList([nn.Conv2d(context_dims[i], args.hidden_dims[i] * 3, kernel_size=3,
                                                           padding=1) for i in range(self.args.n_gru_layers)])
-        self.feature = feature if feature is not None else SyntheticFeature(args)
+        if feature is None:
+            # the reference always builds the real backbone (core/foundation_stereo.py:143); here
+            # args.backbone == "real" does (Feature, EdgeNeXt-S + DepthAnythingV2 on the HIP engine), the
+            # default keeps the seeded synthetic stand-in of the north-star benchmark (backbone excluded)
+            feature = Feature(args) if args.get("backbone", "synthetic") == "real" else SyntheticFeature(args)
+        self.feature = feature
         self.proj_cmb = nn.Conv2d(self.feature.d_out[0], 12, kernel_size=1, padding=0)
         self.stem_2 = nn.Sequential(BasicConv_IN(3, 32, kernel_size=3, stride=2, padding=1),
                                     nn.Conv2d(32, 32, 3, 1, 1, bias=False), nn.InstanceNorm2d(32), nn.ReLU())

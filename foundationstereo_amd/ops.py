@@ -1025,3 +1025,178 @@ def timer_query(kernel: str):
     _lib.check(_lib.load().fsmi_timer_query(_lib.KERNELS.index(kernel), ctypes.byref(tot), ctypes.byref(cnt)),
                "timer_query")
     return tot.value, cnt.value
+
+
+# ---------------------------------------------------------------- backbone (csrc/backbone.hip)
+
+def channel_layernorm(x: Tensor, weight: Tensor = None, bias: Tensor = None, eps: float = 1e-6, n: int = None,
+                      out: Tensor = None, x_offset: int = 0) -> Tensor:
+    """LayerNorm over channels of every token: x (B, C, Tx, ...) with the trailing dims flattened to the
+    token axis; tokens [x_offset, x_offset + n) -> out (B, C, To) (default To = n, allocated).
+    nn.LayerNorm of the reference's token-major (B, T, C) tensors (dinov2 layers/block.py:63,75) and
+    LayerNorm2d / channels-last LayerNorm of NCHW maps."""
+    _check("channel_layernorm", x, *[t for t in (weight, bias) if t is not None])
+    B, C = x.shape[:2]
+    x = _c(x)
+    Tx = x[0, 0].numel()
+    n = Tx - x_offset if n is None else n
+    assert 0 < n and x_offset + n <= Tx, f"channel_layernorm: tokens [{x_offset}, {x_offset + n}) of {Tx}"
+    if out is None:
+        out = torch.empty((B, C, n), device=x.device, dtype=torch.float32)
+    _check("channel_layernorm", out)
+    assert out.is_contiguous() and out.shape[:2] == (B, C)
+    To = out[0, 0].numel()
+    assert To >= n
+    w = _c(weight.detach().float()) if weight is not None else None
+    b = _c(bias.detach().float()) if bias is not None else None
+    _lib.check(_lib.load().fsmi_channel_layernorm(_p(x) + 4 * x_offset, _p(out), _p(w) if w is not None else None,
+                                                  _p(b) if b is not None else None, B, C, Tx, To, n, float(eps),
+                                                  _stream(x)), "channel_layernorm")
+    return out
+
+
+def vit_attention(qkv: Tensor, heads: int, T: int, scale: float, out: Tensor = None) -> Tensor:
+    """Multi-head softmax(q k^T * scale) v (dinov2 layers/attention.py:69-79) on the channel-major qkv
+    (B, 3*heads*64, Tp) of the qkv 1x1 conv; keys >= T masked -> (B, heads*64, Tp)."""
+    _check("vit_attention", qkv)
+    B, C3 = qkv.shape[:2]
+    qkv = _c(qkv)
+    Tp = qkv[0, 0].numel()
+    hd = C3 // (3 * heads)
+    assert C3 == 3 * heads * hd
+    if out is None:
+        out = torch.empty((B, heads * hd) + tuple(qkv.shape[2:]), device=qkv.device, dtype=torch.float32)
+    _check("vit_attention", out)
+    _lib.check(_lib.load().fsmi_vit_attention(_p(qkv), _p(out), B, heads, hd, int(T), Tp, float(scale),
+                                              _stream(qkv)), "vit_attention")
+    return out
+
+
+def space_to_depth(x: Tensor, k: int) -> Tensor:
+    """(B, C, H, W) -> (B, C*k*k, H/k, W/k), channel (c*k + ky)*k + kx: a stride == kernel conv's im2col."""
+    _check("space_to_depth", x)
+    B, C, H, W = x.shape
+    x = _c(x)
+    out = torch.empty((B, C * k * k, H // k, W // k), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_space_to_depth(_p(x), _p(out), B, C, H, W, k, _stream(x)), "space_to_depth")
+    return out
+
+
+def depth_to_space(x: Tensor, k: int) -> Tensor:
+    """(B, k*k*C, H, W) with channel (ky*k + kx)*C + c -> (B, C, H*k, W*k)."""
+    _check("depth_to_space", x)
+    B, CK, H, W = x.shape
+    assert CK % (k * k) == 0
+    C = CK // (k * k)
+    x = _c(x)
+    out = torch.empty((B, C, H * k, W * k), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_depth_to_space(_p(x), _p(out), B, C, H, W, k, _stream(x)), "depth_to_space")
+    return out
+
+
+def vit_tokens(emb: Tensor, cls: Tensor, pos: Tensor, Tp: int) -> Tensor:
+    """[patch embeddings; class token; 0 ...] + position embedding -> (B, C, Tp) (patches first)."""
+    _check("vit_tokens", emb, cls, pos)
+    B, C = emb.shape[:2]
+    emb = _c(emb)
+    N = emb[0, 0].numel()
+    assert cls.numel() == C and tuple(pos.shape) == (C, Tp), f"vit_tokens: pos {tuple(pos.shape)} for ({C}, {Tp})"
+    cls, pos = _c(cls), _c(pos)
+    out = torch.empty((B, C, Tp), device=emb.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_vit_tokens(_p(emb), _p(cls), _p(pos), _p(out), B, C, N, Tp, _stream(emb)),
+               "vit_tokens")
+    return out
+
+
+def resize_bicubic(x: Tensor, size) -> Tensor:
+    """``F.interpolate(x, size, mode="bicubic", align_corners=False)`` (core/extractor.py:352)."""
+    _check("resize_bicubic", x)
+    B, C, Hi, Wi = x.shape
+    Ho, Wo = size
+    x = _c(x)
+    out = torch.empty((B, C, Ho, Wo), device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_resize_bicubic(_p(x), _p(out), B, C, Hi, Wi, Ho, Wo, _stream(x)), "resize_bicubic")
+    return out
+
+
+_IN_ACT = {None: 0, "none": 0, "relu": 1, "leaky": 6}
+
+
+def instance_norm(x: Tensor, act=None, res: Tensor = None, act2=None, eps: float = 1e-5, out: Tensor = None) -> Tensor:
+    """``act2(act(InstanceNorm2d(x)) + res)`` (no affine, biased variance) per (b, c) plane."""
+    _check("instance_norm", x, *([res] if res is not None else []))
+    x = _c(x)
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    if res is not None:
+        res = _c(res)
+        assert res.shape == x.shape
+    out = torch.empty_like(x) if out is None else out
+    _lib.check(_lib.load().fsmi_instance_norm(_p(x), _p(res) if res is not None else None, _p(out), B * C, HW,
+                                              float(eps), _IN_ACT[act], _IN_ACT[act2], _stream(x)), "instance_norm")
+    return out
+
+
+_EW = {"add": 0, "relu": 1, "add_relu": 2, "mul": 3}
+
+
+def elementwise(a: Tensor, b: Tensor = None, op: str = "add", broadcast: bool = False, out: Tensor = None) -> Tensor:
+    """``a + b`` / ``relu(a)`` / ``relu(a + b)`` / ``a * b``; ``broadcast``: b holds one image, repeated
+    over a's batch."""
+    _check("elementwise", a, *([b] if b is not None else []))
+    a = _c(a)
+    bper = 0
+    if b is not None:
+        b = _c(b)
+        if broadcast:
+            bper = b.numel()
+            assert a.numel() % bper == 0
+        else:
+            assert b.numel() == a.numel()
+    out = torch.empty_like(a) if out is None else out
+    _lib.check(_lib.load().fsmi_elementwise(_p(a), _p(b) if b is not None else None, _p(out), a.numel(), bper,
+                                            _EW[op], _stream(a)), "elementwise")
+    return out
+
+
+def xca(qkv: Tensor, temperature: Tensor, heads: int) -> Tensor:
+    """EdgeNeXt cross-covariance attention core on the channel-major qkv (B, 3C, H, W) -> (B, C, H, W)."""
+    t = _c(temperature.detach().float().reshape(-1))
+    _check("xca", qkv, t)
+    B, C3 = qkv.shape[:2]
+    C = C3 // 3
+    qkv = _c(qkv)
+    N = qkv[0, 0].numel()
+    ch = C // heads
+    ws = torch.empty(B * heads * ch * ch, device=qkv.device, dtype=torch.float32)
+    out = torch.empty((B, C) + tuple(qkv.shape[2:]), device=qkv.device, dtype=torch.float32)
+    _lib.check(_lib.load().fsmi_xca(_p(qkv), _p(t), _p(ws), _p(out), B, C, heads, N, _stream(qkv)), "xca")
+    return out
+
+
+def dwconv2d_ex(x, w: Tensor, bias: Tensor = None, add=None, out=None) -> Tensor:
+    """Depthwise KSxKS conv (KS 3/5/7/9, 'same') on channel slices: ``x`` / ``add`` / ``out`` are tensors
+    or (tensor, c0, n) slices of contiguous NCHW maps; out = conv(x + add) + bias."""
+    def sl(s):
+        return (s, 0, s.shape[1]) if isinstance(s, torch.Tensor) else s
+    xt, xc0, C = sl(x)
+    _check("dwconv2d_ex", xt, w, *([bias] if bias is not None else []))
+    B, Cx, H, W = xt.shape
+    KS = w.shape[-1]
+    assert w.shape == (C, 1, KS, KS) and xt.is_contiguous(), f"dwconv2d_ex: weight {tuple(w.shape)} for {C} channels"
+    if add is not None:
+        at, ac0, an = sl(add)
+        assert an == C and at.is_contiguous() and at.shape[2:] == (H, W)
+        _check("dwconv2d_ex", at)
+    if out is None:
+        out = (torch.empty((B, C, H, W), device=xt.device, dtype=torch.float32), 0, C)
+    ot, oc0, on = sl(out)
+    assert on == C and ot.is_contiguous() and ot.shape[2:] == (H, W)
+    HW = H * W
+    w = _c(w.detach().float())
+    b = _c(bias.detach().float()) if bias is not None else None
+    _lib.check(_lib.load().fsmi_dwconv2d_ex(
+        _p(xt) + 4 * xc0 * HW, Cx, (_p(at) + 4 * ac0 * HW) if add is not None else None,
+        at.shape[1] if add is not None else C, _p(w), _p(b) if b is not None else None, _p(ot) + 4 * oc0 * HW,
+        ot.shape[1], B, C, KS, H, W, _stream(xt)), "dwconv2d_ex")
+    return ot

@@ -140,9 +140,23 @@ def conv_any(conv, x):
 
 
 def run_seq(seq, x):
-    """nn.Sequential forward with its bare Conv2d layers through ``conv_any``."""
-    for m in seq:
-        x = conv_any(m, x) if type(m) is nn.Conv2d else m(x)
+    """nn.Sequential forward with its bare Conv2d layers through ``conv_any`` and its InstanceNorm2d
+    (+ a following ReLU / LeakyReLU) through ``ops.instance_norm``."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if type(m) is nn.Conv2d:
+            x = conv_any(m, x)
+        elif _hip_in(m, x):
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            act = "relu" if type(nxt) is nn.ReLU else ("leaky" if type(nxt) is nn.LeakyReLU
+                                                       and nxt.negative_slope == 0.01 else None)
+            x = ops.instance_norm(_f32(x), act=act, eps=m.eps)
+            i += act is not None
+        else:
+            x = m(x)
+        i += 1
     return x
 
 
@@ -212,6 +226,25 @@ def _fast2d(x, conv, bn) -> bool:
         return False
     return bn is None or isinstance(bn, nn.Identity) or (type(bn) is nn.BatchNorm2d and not bn.training
                                                          and bn.track_running_stats)
+
+
+def _hip_in(norm, x) -> bool:
+    """An eval-style InstanceNorm2d (no affine, no running statistics: nn.InstanceNorm2d's defaults, as
+    every InstanceNorm of the reference) that ``ops.instance_norm`` runs."""
+    return (type(norm) is nn.InstanceNorm2d and not norm.affine and not norm.track_running_stats and x.is_cuda
+            and x.dtype in HIP_DTYPES and x.dim() == 4 and not torch.is_grad_enabled() and FILTER3D)
+
+
+def _conv2d_hip(conv, x):
+    """A bare Conv2d / ConvTranspose2d(k4 s2 p1) on the HIP conv engine, or None when it does not apply."""
+    if type(conv) is nn.Conv2d:
+        if _fast2d(x, conv, None):
+            return conv2d_bn_act([x], conv, None)
+        if _fast_s2_2d(x, conv, None):
+            return conv2d_s2_bn_act(x, conv, None)
+    elif fast_up2d(x, conv, None):
+        return deconv2d_bn_act(x, conv)
+    return None
 
 
 def _packed_bn(conv, bn):
@@ -284,6 +317,10 @@ class BasicConv(nn.Module):
             return conv2d_bn_act([x], self.conv, bn, "leaky" if self.relu else None)
         if fast_up2d(x, self.conv, bn):             # ConvTranspose2d k4 s2: 4 phase convs, BN folded
             return deconv2d_bn_act(x, self.conv, bn, "leaky" if self.relu else None)
+        if bn is not None and _hip_in(bn, x):       # norm='instance': conv, then InstanceNorm + LeakyReLU
+            y = _conv2d_hip(self.conv, x)
+            if y is not None:
+                return ops.instance_norm(y, act="leaky" if self.relu else None, eps=bn.eps)
         x = self.bn(self.conv(x)) if self.use_bn else self.conv(x)
         return F.leaky_relu(x, 0.01) if self.relu else x
 
@@ -347,6 +384,12 @@ class _ResBlock(nn.Module):
             y = conv3d_bn_act(x, self.conv1, bn1, "relu")
             # relu(bn2(conv2) + x) [* sigmoid(fatt)]
             return conv3d_bn_act(y, self.conv2, bn2, "relu", res=x, res_pre=True, fatt=fatt)
+        if (self.downsample is None and fatt is None and bn1 is not None and _hip_in(bn1, x) and _hip_in(bn2, x)
+                and _fast2d(x, self.conv1, None) and _fast2d(x, self.conv2, None)):
+            # InstanceNorm variant (Conv2x_IN's conv2): relu(IN(conv2(relu(IN(conv1 x)))) + x)
+            x = _f32(x)
+            y = ops.instance_norm(conv2d_bn_act([x], self.conv1, None), act="relu", eps=bn1.eps)
+            return ops.instance_norm(conv2d_bn_act([y], self.conv2, None), res=x, act2="relu", eps=bn2.eps)
         if fatt is not None:
             return torch.sigmoid(fatt).unsqueeze(2) * self.forward(x)
         y = self.conv1(x)
@@ -491,6 +534,10 @@ class BasicConv_IN(nn.Module):
         self.IN = nn.InstanceNorm3d(out_channels) if is_3d else nn.InstanceNorm2d(out_channels)
 
     def forward(self, x):
+        if self.use_in and _hip_in(self.IN, x):
+            y = _conv2d_hip(self.conv, x)
+            if y is not None:
+                return ops.instance_norm(y, act="leaky" if self.relu else None, eps=self.IN.eps)
         x = conv_any(self.conv, x)
         if self.use_in:
             x = self.IN(x)

@@ -324,6 +324,52 @@ int fsmi_disparity_transformer(const float* x, float* out, const float* params, 
                                int L, int HW, int nheads, int ffdim, int nlayers, float eps, void* stream);
 int fsmi_upsample4_add(const float* t, float* vol, int B, int C, int D, int H, int W, void* stream);
 
+/* ---- backbone: DepthAnythingV2 ViT + DPT, EdgeNeXt-S, Feature fusion --------
+ * replaces Feature / DepthAnythingFeature (core/extractor.py:286-369), the DINOv2 ViT
+ * (dinov2/dinov2/models/vision_transformer.py, layers/{attention,block,patch_embed}.py), the DPT head
+ * (depth_anything/dpt.py:24-190, depth_anything/blocks.py) and timm's edgenext_small (core/extractor.py:327).
+ * The ViT runs on the channel-major token layout (B, C, Tp): token t of channel c at c*Tp + t, the N patch
+ * tokens first, the class token at N, zero padding up to Tp; every Linear is then a 1x1 conv of
+ * fsmi_conv2d_halo_x3 over a (Tp/32) x 32 "image".
+ * fsmi_channel_layernorm: nn.LayerNorm over channels per token (eps), x (B,C,Tx) -> out (B,C,To), tokens
+ *   [0, n) (n <= Tx, To); w / b (C) or NULL.  Also LayerNorm2d / channels-last LayerNorm of NCHW maps
+ *   (Tx = To = n = H*W).
+ * fsmi_vit_attention: softmax(q k^T * scale) v per head (layers/attention.py:69-79): qkv (B, 3*heads*64, Tp)
+ *   = [q; k; v] channel-major, out (B, heads*64, Tp); keys >= T masked; head_dim 64; Tp % 64 == 0.
+ *   Split-precision MFMA (3 fp16 products per MAC), fp32 softmax.
+ * fsmi_space_to_depth: out[b, (c*k+ky)*k+kx, y, x] = x[b, c, y*k+ky, x*k+kx] (B,C,H,W) -> (B,C*k*k,H/k,W/k):
+ *   the im2col of a conv with stride == kernel (patch embed k14, EdgeNeXt stem k4 / downsample k2).
+ * fsmi_depth_to_space: out[b, c, y*k+ky, x*k+kx] = x[b, (ky*k+kx)*C + c, y, x]: a ConvTranspose2d with
+ *   stride == kernel (DPT resize_layers[0..1]) after its 1x1-conv form.
+ * fsmi_vit_tokens: out[b,c,t] = (emb[b,c,t] for t < N | cls[c] for t == N | 0) + pos[c,t] (pos (C,Tp), zero
+ *   past N): prepare_tokens_with_masks (vision_transformer.py:214-233) in the layout above.
+ * fsmi_resize_bicubic: F.interpolate(mode="bicubic", align_corners=False), A = -0.75, border-clamped taps
+ *   (core/extractor.py:352).
+ * fsmi_instance_norm: out = act2(act1(InstanceNorm(x)) + res) per plane (planes = B*C, biased variance, no
+ *   affine), res may be NULL; act 0 none, 1 ReLU, 6 LeakyReLU(0.01) (core/submodule.py:320-385,
+ *   core/extractor.py:20-80 with norm 'instance').
+ * fsmi_elementwise: op 0 a+b, 1 relu(a), 2 relu(a+b), 3 a*b; b indexed modulo bper when bper > 0.
+ * fsmi_xca: EdgeNeXt cross-covariance attention core (timm CrossCovarianceAttn): qkv (B,3C,N) channel-major,
+ *   temperature (heads), attn_ws (B*heads*(C/heads)^2 floats), out (B,C,N); C/heads <= 40.
+ * fsmi_dwconv2d_ex: fsmi_dwconv2d on channel slices (x / add / out planes at (b*ctot + c)*H*W), KS in
+ *   {3,5,7,9}, with add (or NULL) summed into the input first. */
+int fsmi_channel_layernorm(const float* x, float* out, const float* w, const float* b, int B, int C, int Tx, int To,
+                           int n, float eps, void* stream);
+int fsmi_vit_attention(const float* qkv, float* out, int B, int heads, int head_dim, int T, int Tp, float scale,
+                       void* stream);
+int fsmi_space_to_depth(const float* x, float* out, int B, int C, int H, int W, int k, void* stream);
+int fsmi_depth_to_space(const float* x, float* out, int B, int C, int H, int W, int k, void* stream);
+int fsmi_vit_tokens(const float* emb, const float* cls, const float* pos, float* out, int B, int C, int N, int Tp,
+                    void* stream);
+int fsmi_resize_bicubic(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
+int fsmi_instance_norm(const float* x, const float* res, float* out, int planes, int HW, float eps, int act1, int act2,
+                       void* stream);
+int fsmi_elementwise(const float* a, const float* b, float* out, long long n, long long bper, int op, void* stream);
+int fsmi_xca(const float* qkv, const float* temperature, float* attn_ws, float* out, int B, int C, int heads, int N,
+             void* stream);
+int fsmi_dwconv2d_ex(const float* x, int x_ctot, const float* add, int add_ctot, const float* w, const float* bias,
+                     float* out, int out_ctot, int B, int C, int KS, int H, int W, void* stream);
+
 /* ---- live kernel timing (bench.py roofline) -----------------------------
  * When enabled, every launch of the kernels below is bracketed by a pair of
  * hipEvents recorded on the launch stream (skipped while the stream is being

@@ -73,3 +73,22 @@ def test_unexpected_non_backbone_key_is_an_error(tmp_path):
     path, _ = _write(tmp_path, extra={"update_block.bogus.weight": torch.zeros(3)})
     with pytest.raises(RuntimeError, match="bogus"):
         load_model(path)
+
+
+def test_backbone_keys_load_into_real_feature(tmp_path):
+    """With the real backbone (backbone=True) the checkpoint's feature.* weights load strictly."""
+    from foundationstereo_amd.foundation_stereo import FoundationStereo
+    args = synth.make_args(max_disp=64, corr_levels=2, vit_size="vits")
+    args["backbone"] = "real"
+    m = FoundationStereo(args)
+    synth.init_module_(m, seed=7)
+    path = os.path.join(tmp_path, "model_best_bp2.pth")
+    torch.save({"model": m.state_dict(), "global_step": 1, "epoch": 0}, path)
+    cfg = {k: v for k, v in args.items() if k != "backbone"}
+    with open(os.path.join(tmp_path, "cfg.yaml"), "w") as f:
+        yaml.safe_dump(cfg, f)
+    model, meta = load_model(path, backbone=True)
+    assert meta["skipped_backbone_keys"] == []
+    a, b = model.state_dict(), m.state_dict()
+    assert list(a) == list(b) and any(k.startswith("feature.dino.") for k in a)
+    assert all(torch.equal(a[k], b[k]) for k in a)

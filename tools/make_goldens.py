@@ -24,7 +24,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
 from foundationstereo_amd import synth  # noqa: E402
-from ref_harness import import_reference, make_synthetic_feature_class  # noqa: E402
+from ref_harness import import_reference, import_reference_extractor, make_synthetic_feature_class  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden")
 torch.set_num_threads(8)
@@ -199,10 +199,59 @@ def hiera(fs):
         print(name, "disp", tuple(out.shape), "mean", float(out.mean()))
 
 
+BACKBONE_CASES = {
+    # name: (encoder, input shape) -- DepthAnythingFeature on an already /14 input
+    "dav2_vits": ("vits", (2, 3, 56, 70)),
+    "dav2_vitl": ("vitl", (1, 3, 28, 42)),
+}
+FEATURE_CASES = {"feature_vits": ("vits", (2, 3, 64, 96))}
+
+
+def backbone():
+    """DepthAnythingFeature (core/extractor.py:286-320) and Feature (:323-369) run by the reference,
+    hash-initialised; inputs from synth (regenerated by the tests)."""
+    ext = import_reference_extractor()
+    for name, (enc, shape) in BACKBONE_CASES.items():
+        m = ext.DepthAnythingFeature(encoder=enc).eval()
+        synth.init_module_(m, seed=4321)
+        x = synth.normal(synth.name_seed(name + "_x"), shape)
+        with torch.no_grad():
+            out = m(t(x))
+        g = {k: out[k].numpy() for k in ("out", "path_1", "path_2", "path_3", "path_4", "disp")}
+        for i, (tok, cls) in enumerate(out["features"]):
+            g[f"feat{i}"], g[f"cls{i}"] = tok.numpy(), cls.numpy()
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **g)
+        with open(os.path.join(OUT, f"state_dict_{name}.json"), "w") as f:
+            json.dump([[k, list(v.shape)] for k, v in m.state_dict().items()], f)
+        print(name, {k: v.shape for k, v in g.items()})
+    for name, (vit, shape) in FEATURE_CASES.items():
+        args = synth.make_args(vit_size=vit)
+        m = ext.Feature(args).eval()
+        synth.init_module_(m, seed=4321)
+        x = synth.normal(synth.name_seed(name + "_x"), shape)
+        with torch.no_grad():
+            feats, vit_feat = m(t(x))
+        g = {f"x{4 << i}": f.numpy() for i, f in enumerate(feats)}
+        g["vit_feat"] = vit_feat.numpy()
+        np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **g)
+        with open(os.path.join(OUT, f"state_dict_{name}.json"), "w") as f:
+            json.dump([[k, list(v.shape)] for k, v in m.state_dict().items()], f)
+        print(name, {k: v.shape for k, v in g.items()})
+    # the whole model with its real backbone: the checkpoint layout (feature.* included)
+    fs, *_ = import_reference()
+    fs.Feature = ext.Feature
+    for vit in ("vits", "vitl"):
+        m = fs.FoundationStereo(synth.make_args(max_disp=192, corr_levels=4, vit_size=vit))
+        with open(os.path.join(OUT, f"state_dict_full_{vit}.json"), "w") as f:
+            json.dump([[k, list(v.shape)] for k, v in m.state_dict().items()], f)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fs, sm, geo_mod, up_mod, ut = import_reference()
-    which = sys.argv[1:] or ["ops", "update", "e2e", "hiera"]
+    which = sys.argv[1:] or ["ops", "update", "e2e", "hiera", "backbone"]
+    if "backbone" in which:
+        backbone()
     if "hiera" in which:
         hiera(fs)
     if "ops" in which:

@@ -5,11 +5,13 @@ the product, the GPU tests, ``smoke()`` or ``bench.py`` (the reference does not
 exist on the GPU box).
 
 Absent third-party modules that carry no hot-path arithmetic are stubbed
-(SURVEY.md §8c): open3d, trimesh, transformations, imageio, timm, cv2,
+(SURVEY.md §8c): open3d, trimesh, transformations, imageio, cv2,
 torchvision (``transforms.Normalize`` only) and flash_attn (``flash_attn_func``
 restated as non-causal SDPA with the default 1/sqrt(head_dim) scale, the same
-math as the reference's call at ``core/submodule.py:224``).  The backbone
-``Feature`` (remote timm / torch.hub weights) is replaced by a synthetic source.
+math as the reference's call at ``core/submodule.py:224``).  For the stereo goldens the backbone
+``Feature`` (remote timm / torch.hub weights) is replaced by a synthetic source; for the backbone
+goldens ``torch.hub.load`` builds DINOv2 from the vendored ``dinov2/`` (pretrained=False) and
+``timm.create_model('edgenext_small')`` returns tools/edgenext_timm.py's restatement (no weights).
 """
 from __future__ import annotations
 
@@ -32,9 +34,17 @@ def install_stubs():
     import torch
     import torch.nn.functional as F
 
-    for n in ("open3d", "trimesh", "transformations", "imageio", "timm"):
+    for n in ("open3d", "trimesh", "transformations", "imageio"):
         if n not in sys.modules:
             _stub(n)
+    if "timm" not in sys.modules:
+        # core/extractor.py:327 timm.create_model('edgenext_small', pretrained=True): answered by the
+        # module-form restatement of timm's published edgenext_small (tools/edgenext_timm.py; no weights)
+        def create_model(*a, **k):
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            import edgenext_timm
+            return edgenext_timm.create_model(*a, **k)
+        _stub("timm", create_model=create_model)
     if "cv2" not in sys.modules:
         _stub("cv2", COLORMAP_TURBO=20, COLORMAP_JET=2)
 
@@ -60,6 +70,22 @@ def install_stubs():
               flash_attn_qkvpacked_func=lambda *a, **k: (_ for _ in ()).throw(NotImplementedError()))
 
 
+def install_hub_stub():
+    """depth_anything/dpt.py:159 fetches DINOv2 with torch.hub.load('facebookresearch/dinov2', ...) (remote);
+    answer it from the vendored copy in the reference, the way dinov2/hub/backbones.py:18-61 builds the
+    model (pretrained=False: no weight download)."""
+    import torch
+    if os.path.join(REF_ROOT, "dinov2") not in sys.path:
+        sys.path.insert(0, os.path.join(REF_ROOT, "dinov2"))
+    from dinov2.hub import backbones
+
+    def hub_load(repo, model, *a, pretrained=True, **k):
+        assert repo == "facebookresearch/dinov2", repo
+        return getattr(backbones, model)(pretrained=False, **k)
+
+    torch.hub.load = hub_load
+
+
 def import_reference():
     """Return the reference modules ``(foundation_stereo, submodule, geometry, update, utils)``."""
     sys.dont_write_bytecode = True
@@ -74,6 +100,14 @@ def import_reference():
     up = importlib.import_module("core.update")
     ut = importlib.import_module("core.utils.utils")
     return fs, sm, geo, up, ut
+
+
+def import_reference_extractor():
+    """The reference ``core.extractor`` (Feature, DepthAnythingFeature) with the hub / timm stand-ins."""
+    import_reference()
+    install_hub_stub()
+    import importlib
+    return importlib.import_module("core.extractor")
 
 
 def make_synthetic_feature_class(feature_dims_fn):
