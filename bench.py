@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the FoundationStereo hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2] [--with-backbone]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
@@ -9,7 +9,8 @@ A step = one ``FoundationStereo.forward(test_mode=True)`` over this rank's
 pairs: cost-volume build, 3D filtering, context net, geometry encoding, 32
 refinement iterations (lookup + ConvGRU update), convex upsampling.  Inputs
 (images and the synthetic backbone's feature maps) are resident
-in HBM before the timed region; the out-of-scope backbone is not run.
+in HBM before the timed region; the backbone is not run (``--with-backbone``: a secondary line
+whose timed forward also runs the real ``Feature`` on the HIP engine).
 Multi-GPU: rank 0 scatters each rank its shard of the image batch every step
 and the disparities are all-gathered back (RCCL over xGMI), weights broadcast
 once.
@@ -105,7 +106,8 @@ def make_model(args, device, rank):
 
 def cpu_baseline(args, H, W, iters, threads, hiera=False, pair=0):
     """Time the CPU oracle on one pair of the same workload on the host cores: global pair ``pair``
-    of the bench's batch (images and backbone features seeded 0x5EED + pair, as the ranks make them)."""
+    of the bench's batch (images and backbone features seeded 0x5EED + pair, as the ranks make them;
+    with ``args.backbone == "real"`` the features come from the oracle's backbone restatement)."""
     import oracle
     torch.set_num_threads(threads)
     from foundationstereo_amd.foundation_stereo import FoundationStereo
@@ -117,7 +119,16 @@ def cpu_baseline(args, H, W, iters, threads, hiera=False, pair=0):
     T = oracle.StageTimer()
     t0 = time.perf_counter()
     with torch.no_grad():
-        if hiera:
+        if args.get("backbone") == "real" and not hiera:
+            from oracle import backbone_oracle
+            T.mark("backbone")
+            mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+            std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+            ims = (torch.from_numpy(np.concatenate([left, right])) / 255.0 - mean) / std
+            feats, vf = backbone_oracle.feature_forward(P, "feature.", ims, args.vit_size)
+            out = oracle.oracle_forward(P, args, torch.from_numpy(left), torch.from_numpy(right),
+                                        [f[:1] for f in feats], [f[1:] for f in feats], vf[:1], iters=iters, timer=T)
+        elif hiera:
             def features(B, h, w):
                 fl, fr, vf = synth.backbone_features(B, h, w, args.vit_size, seed=seed, shift_px=8)
                 return [torch.from_numpy(a) for a in fl], [torch.from_numpy(a) for a in fr], torch.from_numpy(vf)
@@ -199,12 +210,14 @@ def dist_selftest(a):
         runner.step(batch, (1, H, W))
     if world > 1:
         torch.distributed.barrier()
+    runner.timing = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         out = runner.step(batch, (1, H, W))
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    attribution = fdist.rank_attribution(runner, elapsed, a.steps, torch.device("cpu"))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -216,7 +229,7 @@ def dist_selftest(a):
                               "the stand-in function on the host")
         print(json.dumps({"metric": "dist self-test (no model)", "value": a.steps * B / elapsed, "unit": "pairs/s",
                           "n_gpus": wsz, "world_size": wsz, "backend": backend, "steps": a.steps,
-                          "warmup": a.warmup, "gathered_ok": ok, "parity": parity,
+                          "warmup": a.warmup, "gathered_ok": ok, "parity": parity, **attribution,
                           "data": "dist self-test: stand-in per-pair function on CPU tensors, not a measurement"}),
               flush=True)
     if world > 1:
@@ -247,6 +260,10 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="create the torch.distributed process group (RCCL) even at one rank, so the step's "
                          "scatter / all-gather run as collectives")
+    ap.add_argument("--with-backbone", action="store_true",
+                    help="secondary line: the timed forward also runs the real backbone (Feature: EdgeNeXt-S + "
+                         "DepthAnythingV2 ViT + DPT, core/extractor.py:323-369) on the HIP engine instead of "
+                         "reading preset features (the headline stays backbone-excluded, as north_star names)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU/gloo self-test of the rank launch and sharding machinery (no model, not a measurement)")
     a = ap.parse_args()
@@ -273,6 +290,10 @@ def main():
         per_gpu = a.pairs_per_gpu
     L = a.corr_levels
     args = synth.make_args(max_disp=md, corr_levels=L, vit_size=vit, mixed_precision=a.mixed_precision)
+    if a.with_backbone:
+        if a.config in HIERA:
+            raise SystemExit("bench.py: --with-backbone is for the single-pass configs")
+        args["backbone"] = "real"
     model = make_model(args, device, rank)
 
     from foundationstereo_amd import _lib, ops
@@ -281,7 +302,7 @@ def main():
     lo, hi = fdist.shard_range(B, rank, world)
     # this rank's backbone output, resident in HBM (seed = 0x5EED + global pair index), per pass size
     sizes = pass_sizes(a.config, H, W)
-    for (ph, pw) in sizes:
+    for (ph, pw) in ([] if a.with_backbone else sizes):
         feats = [synth.backbone_features(1, ph, pw, vit, seed=0x5EED + i, shift_px=8) for i in range(lo, hi)]
         fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(device) for j in range(4)]
         fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(device) for j in range(4)]
@@ -332,6 +353,7 @@ def main():
         ops.timer_reset()
     if world > 1:
         torch.distributed.barrier()
+        runner.timing = []          # per-rank scatter / forward / all-gather spans (events, no sync)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -340,6 +362,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    attribution = fdist.rank_attribution(runner, elapsed, a.steps, device) if world > 1 else {}
+    runner.timing = None
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -451,7 +475,8 @@ def main():
                   "f32 (3xfp16 split MFMA convs; library convs fp16 under autocast)" if a.mixed_precision
                   else "f32 (3xfp16 split MFMA)"),
         "precision": a.precision,
-        "data": "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)",
+        "data": ("synthetic (hash-PRNG images, hash-init weights incl. the backbone)" if a.with_backbone else
+                 "synthetic (hash-PRNG images + synthetic backbone features, hash-init weights)"),
         "range_overflow": range_overflow,             # set during the timed replays
         "range_overflow_timing_pass": range_overflow_eager,
         "output_finite": out_finite,
@@ -459,7 +484,10 @@ def main():
         "range_recoveries": ops.RANGE_RECOVERIES[0],
         "config": {"workload": f"{a.config}: {W}x{H}{' hierarchical' if a.config in HIERA else ''}, "
                                f"max_disp {md}, {iters} iters, {vit}, "
-                               f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward excl. backbone",
+                               f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward "
+                               + ("INCL. backbone (Feature on HIP; secondary line)" if a.with_backbone
+                                  else "excl. backbone"),
+                   "backbone": "real" if a.with_backbone else "preset features (excluded)",
                    "global_batch": B, "resolution": f"{W}x{H}", "max_disp": md, "iters": iters,
                    "corr_levels": L, "conv_engine": a.conv_engine, "hip_graph": bool(a.graph),
                    "parallelism": f"dp{world}"},
@@ -467,6 +495,9 @@ def main():
         # to last wave end, baked into the captured graph: the last timed replay's launches, beside the
         # other streams' kernels that share the chip and its HBM); the single-stream eager pass after
         # the timed region is kept as a secondary figure
+        # N > 1: each rank's own step time and its scatter / forward / all-gather split (max over ranks
+        # is `ms_per_step`); the world size every rank's process group reported
+        **({"rank_attribution": attribution} if attribution else {}),
         "roofline": {"kernel": "geo_lookup", "bound": "hbm",
                      "timed_over": ("the timed step (last replay's launches)" if lk_head_in_step else
                                     "single-stream eager step after the timed region" if a.graph else "timed region"),

@@ -110,6 +110,39 @@ class ShardedStereo:
         # after each replay: synchronise, read the range flag, recover in safe mode (True); or leave
         # it to the graph's NaN fill and the caller's ops.check_range(), with no host sync (False)
         self.recover = True
+        # per-phase timing of step() (scatter / this rank's forward / all-gather): None = off, else the
+        # marks of each timed step -- HIP events on the current stream (RCCL collectives are ordered
+        # with it), host clocks for host-staged gloo; read with phase_times()
+        self.timing = None
+
+    def _mark(self, dev):
+        if dev.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(dev))
+            return e
+        import time
+        return time.perf_counter()
+
+    @staticmethod
+    def _span_ms(a, b):
+        if isinstance(a, float):
+            return 1e3 * (b - a)
+        return float(a.elapsed_time(b))
+
+    def phase_times(self):
+        """Mean ms per timed step of each phase {"scatter", "run", "allgather", "step"} (synchronises)."""
+        if not self.timing:
+            return {}
+        if torch.cuda.is_available() and not isinstance(self.timing[0][0], float):
+            torch.cuda.synchronize()
+        n = len(self.timing)
+        tot = {"scatter": 0.0, "run": 0.0, "allgather": 0.0, "step": 0.0}
+        for m0, m1, m2, m3 in self.timing:
+            tot["scatter"] += self._span_ms(m0, m1)
+            tot["run"] += self._span_ms(m1, m2)
+            tot["allgather"] += self._span_ms(m2, m3)
+            tot["step"] += self._span_ms(m0, m3)
+        return {k: v / n for k, v in tot.items()}
 
     def _local_buffer(self, batch):
         b = batch.shape[0] // self.world
@@ -183,14 +216,46 @@ class ShardedStereo:
         B = batch.shape[0]
         if B % self.world:
             raise ValueError(f"batch {B} not divisible by world size {self.world}")
+        timed = self.timing is not None
+        dev = batch.device
+        m0 = self._mark(dev) if timed else None
         local = self._scatter(batch)
+        m1 = self._mark(dev) if timed else None
         disp = self._run(local)
+        m2 = self._mark(dev) if timed else None
         if not dist.is_initialized():
-            return disp
-        if _host_staged():
+            out = disp
+        elif _host_staged():
             parts = [torch.empty_like(disp, device="cpu") for _ in range(self.world)]
             dist.all_gather(parts, disp.contiguous().cpu())
-            return torch.cat(parts, 0).to(disp.device)
-        gathered = torch.empty((B,) + tuple(out_shape_per_pair), device=disp.device, dtype=disp.dtype)
-        dist.all_gather_into_tensor(gathered, disp.contiguous())
-        return gathered
+            out = torch.cat(parts, 0).to(disp.device)
+        else:
+            out = torch.empty((B,) + tuple(out_shape_per_pair), device=disp.device, dtype=disp.dtype)
+            dist.all_gather_into_tensor(out, disp.contiguous())
+        if timed:
+            self.timing.append((m0, m1, m2, self._mark(dev)))
+        return out
+
+
+def rank_attribution(runner: ShardedStereo, elapsed_s: float, steps: int, device) -> dict:
+    """Every rank's own timed-region step time and phase split, gathered to all ranks: the fields a
+    multi-GPU line carries so a shortfall from linear scaling can be attributed (a slow rank, the
+    scatter, or the all-gather).  Collective over the group; {} without one."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return {}
+    ph = runner.phase_times()
+    row = [1e3 * elapsed_s / max(steps, 1), ph.get("scatter", 0.0), ph.get("run", 0.0), ph.get("allgather", 0.0),
+           float(dist.get_world_size()), float(dist.get_rank())]
+    host = _host_staged()
+    mine = torch.tensor(row, dtype=torch.float64, device="cpu" if host else device)
+    parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, mine)
+    rows = [p.cpu().tolist() for p in parts]
+    return {"per_rank_ms": [round(r[0], 4) for r in rows],
+            "scatter_ms": [round(r[1], 4) for r in rows],
+            "run_ms": [round(r[2], 4) for r in rows],
+            "allgather_ms": [round(r[3], 4) for r in rows],
+            "rank_world_size": [int(r[4]) for r in rows],
+            "ranks": [int(r[5]) for r in rows],
+            "timed_by": "HIP events on each rank's stream around its scatter / forward / all-gather"
+                        if not host else "host clocks around each rank's scatter / forward / all-gather (gloo)"}

@@ -34,7 +34,7 @@ from .geometry import Combined_Geo_Encoding_Volume
 from .submodule import (BasicConv, BasicConv_IN, ChannelAttentionEnhancement, Conv2x, Conv3dNormActReduced,
                         CostVolumeDisparityAttention, FeatureAtt, ResnetBasicBlock3D, SpatialAttentionExtractor,
                         build_concat_volume, build_gwc_volume)
-from .update import BasicSelectiveMultiUpdateBlock
+from .update import BasicSelectiveMultiUpdateBlock, stream_wait
 from .utils import InputPadder
 
 _MEAN = (0.485, 0.456, 0.406)
@@ -137,7 +137,7 @@ class hourglass(nn.Module):
             # hundred waves) reads only x: it runs on a side stream beside conv1 .. conv1_up
             main = torch.cuda.current_stream(x.device)
             dt_s = _update._side_stream(x.device, 1)
-            dt_s.wait_stream(main)
+            stream_wait(dt_s, main)
             with torch.cuda.stream(dt_s):
                 scale, shift = self._patch_fold()
                 t = self.atts["4"](ops.dt_patch_embed(_sub._f32(x), self.conv_patch[0].weight.float(), scale, shift))
@@ -158,11 +158,11 @@ class hourglass(nn.Module):
             c1 = self.feature_att_up_8(self.agg_1(torch.cat((self.conv2_up(c2), c1), dim=1)), features[1])
         conv = self.conv1_up(c1)
         if dt_s is not None and tuple(conv.shape) == tuple(x.shape):
-            main.wait_stream(dt_s)
+            stream_wait(main, dt_s)
             t.record_stream(main)
             return self.conv_out(ops.upsample4_add_(conv.float().contiguous(), t))
         if dt_s is not None:
-            main.wait_stream(dt_s)
+            stream_wait(main, dt_s)
         if self._dt_fast(x, conv):
             # patch embed, transformer and the x4 trilinear add on HIP (csrc/transformer.hip)
             scale, shift = self._patch_fold()
@@ -329,6 +329,7 @@ class FoundationStereo(nn.Module):
         if not (image1.is_cuda and RANGE_GUARD):
             return run()
         if torch.cuda.is_current_stream_capturing():
+            _update._CAPTURE_EDGES.clear()          # capture_fork: this forward's waits only
             # a captured forward cannot synchronise: its last node NaN-fills the disparity when the
             # flag is set, so a replay that overflowed never returns a finite result (ShardedStereo
             # reads the flag after a replay and recovers)
@@ -361,7 +362,7 @@ class FoundationStereo(nn.Module):
                 # runs them beside the volume build and the 3D filtering (joined before the loop)
                 main = torch.cuda.current_stream(image1.device)
                 ctx_s = _update._side_stream(image1.device, 0)
-                ctx_s.wait_stream(main)
+                stream_wait(ctx_s, main)
                 with torch.cuda.stream(ctx_s):
                     stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
             else:
@@ -372,7 +373,7 @@ class FoundationStereo(nn.Module):
                 # the six FeatureAtt gates (2D 1x1 convs on the features) on a side stream, ready long
                 # before the volume convs that apply them; an event joins only them
                 g_s = _update._side_stream(image1.device, 1)
-                g_s.wait_stream(main)
+                stream_wait(g_s, main)
                 with torch.cuda.stream(g_s):
                     gates = (self.corr_feature_att.logits(features_left[0]),) + \
                         self.cost_agg.gate_logits(features_left)
@@ -398,7 +399,7 @@ class FoundationStereo(nn.Module):
             if ctx_s is not None and not geo_alone:
                 # round-4 schedule (A/B): the geometry pyramids beside the classifier on side stream 1
                 geo_s = _update._side_stream(image1.device, 1)
-                geo_s.wait_stream(main)
+                stream_wait(geo_s, main)
                 with torch.cuda.stream(geo_s):
                     geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(),
                                                           vol.float(), num_levels=self.args.corr_levels, dx=self.dx)
@@ -416,7 +417,7 @@ class FoundationStereo(nn.Module):
                                            head.bias.float()).squeeze(1)
                 init_disp = ops.softmax_regression(logits)
             if ctx_s is not None:
-                main.wait_stream(ctx_s)
+                stream_wait(main, ctx_s)
                 for t in [stem_2x, *net_list, *inp_list, *att]:
                     t.record_stream(main)
 
@@ -424,7 +425,7 @@ class FoundationStereo(nn.Module):
             geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
                                                   num_levels=self.args.corr_levels, dx=self.dx)
         elif geo_s is not None:
-            main.wait_stream(geo_s)
+            stream_wait(main, geo_s)
             for t in [*geo_fn.init_corr_pyramid, *geo_fn.geo_volume_pyramid]:
                 t.record_stream(main)
         disp = init_disp.float()

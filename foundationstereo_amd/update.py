@@ -108,6 +108,49 @@ def _side_stream(device, idx=0):
 # via_main pass).  Hence gru08's small branch on the pipeline stream runs in order, and the motion
 # path's disparity branch forks from main, not from the motion stream.
 #
+#
+# Enforced by ``stream_wait`` (every wait between streams here goes through it): while a capture is in
+# progress it records the waits between side streams and raises before a wait that would close a cycle
+# (X waiting on A after A waited on X, directly or through other side streams) -- every variant the
+# probe saw segfault has such a mutual wait, every variant that passed has none.
+_CAPTURE_EDGES = {}          # id(waiter) -> set of id(waited), side streams only, current capture
+
+
+class CaptureForkError(RuntimeError):
+    """A stream wait that would make hipStreamEndCapture segfault on this ROCm (capture_fork)."""
+
+
+def capture_fork_check(waiter, waited, capturing: bool, side_ids=None):
+    """Record ``waiter`` waiting on ``waited`` for the capture in progress; raise CaptureForkError when
+    ``waited`` already (transitively) waits on ``waiter``.  Only edges between side streams count (the
+    capture origin forks and joins every side stream).  ``side_ids``: ids of the side streams (default
+    the ones ``_side_stream`` made).  Not capturing: forget the edges (a new capture starts clean)."""
+    if not capturing:
+        _CAPTURE_EDGES.clear()
+        return
+    side = side_ids if side_ids is not None else {id(v) for v in _SIDE.values()}
+    a, b = id(waiter), id(waited)
+    if a == b or a not in side or b not in side:
+        return
+    seen, todo = set(), [b]
+    while todo:                                  # does `waited` reach `waiter` through recorded waits?
+        x = todo.pop()
+        if x == a:
+            raise CaptureForkError("capture_fork: a side stream would wait on a side stream that already waits "
+                                   "on it inside this hipGraph capture (hipStreamEndCapture segfaults on this "
+                                   "ROCm; tools/capture_fork_probe.py) -- fork from the capture origin instead")
+        if x not in seen:
+            seen.add(x)
+            todo.extend(_CAPTURE_EDGES.get(x, ()))
+    _CAPTURE_EDGES.setdefault(a, set()).add(b)
+
+
+def stream_wait(waiter, waited):
+    """``waiter.wait_stream(waited)`` with the capture_fork check while a capture is in progress."""
+    capture_fork_check(waiter, waited, torch.cuda.is_current_stream_capturing())
+    waiter.wait_stream(waited)
+
+
 # side stream the SelectiveConvGRU small branch forks to (1); 0: the branches run in order on the
 # caller's stream (run_pipelined: the pipeline stream is itself a side stream, see capture_fork)
 _BRANCH = [1]
@@ -239,7 +282,7 @@ class BasicMotionEncoder(nn.Module):
         if d is None:
             d = self._disp_feat(disp)
         if join is not None:
-            torch.cuda.current_stream(disp.device).wait_stream(join)
+            stream_wait(torch.cuda.current_stream(disp.device), join)
         # cat([cor, dsp]) with the disparity features (~disp magnitude: ~200 at cfg5) as the FIRST
         # segment: the halo conv fixes a block's exponent from its first chunk (conv_halo.h)
         nc, nd = c.shape[1], d.shape[1]
@@ -373,11 +416,11 @@ class SelectiveConvGRU(nn.Module):
                 # large blend adds into ``out`` after the small blend has written it
                 main = torch.cuda.current_stream(h.device)
                 side = _branch_stream(h.device)
-                side.wait_stream(main)
+                stream_wait(side, main)
                 with torch.cuda.stream(side):
                     small()
                 pk, b, z, rh = branch(self.large_gru, "blend_large")
-                main.wait_stream(side)
+                stream_wait(main, side)
                 ops.conv2d_gate([rh, xc], pk, b, "blend_large", h=h, z=z, att=att, out=out)
                 return out
             small()
@@ -443,7 +486,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         side = _side_stream(disp.device)
         B, _, H, W = disp.shape
         enc = disp.new_empty(B, self.encoder.conv.out_channels + 1, H, W)
-        side.wait_stream(main)
+        stream_wait(side, main)
         with torch.cuda.stream(side):
             self.encoder.motion_into(disp, geo_fn, enc)
         n = self.args.n_gru_layers
@@ -454,16 +497,16 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]), interp(net[2], net[1]))
             else:
                 net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]))
-        main.wait_stream(side)
+        stream_wait(main, side)
         if n > 1:
             net[0] = self.gru04(att[0], net[0], inp[0], enc, interp(net[1], net[0]))
         # mask head beside the disparity head (both read net[0] only)
         side1 = _side_stream(disp.device, 1)
-        side1.wait_stream(main)
+        stream_wait(side1, main)
         with torch.cuda.stream(side1):
             mask = _conv(self.mask[2], [_conv(self.mask[0], [net[0]], "relu")], "relu", alpha=0.25)
         delta_disp = self.disp_head(net[0])
-        main.wait_stream(side1)
+        stream_wait(main, side1)
         return net, mask, delta_disp
 
     def run_pipelined(self, net, inp, geo_fn, disp, att, iters):
@@ -476,7 +519,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         disp(t+1)).  The critical path per iteration is gru04 + max(head + motion, gru08) instead of
         gru16 + gru08 + gru04 + head.  Every value is computed by the same kernels from the same
         inputs as ``forward`` (bit-identical); only the order of independent work changes.
-        One pipeline stream and whole-stream joins: ``main.wait_stream(s_gru)`` is issued after
+        One pipeline stream and whole-stream joins: ``stream_wait(main, s_gru)`` is issued after
         gru08(t) and before gru16(t+1) is enqueued, so gru04(t) waits for the former only.  The
         mask head shares the motion stream.  A tensor read on another stream is freed only after
         the freeing stream has joined the reader, so the caching allocator never recycles memory
@@ -488,7 +531,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         n0, n1, n2 = net
         B, _, H, W = disp.shape
         main_branch = PIPE_BRANCH                        # gru04's small branch on stream 1 (4th stream)
-        s_gru.wait_stream(main)
+        stream_wait(s_gru, main)
         _BRANCH[0] = 0                                   # pipeline-stream GRUs: branches in order
         with torch.cuda.stream(s_gru):
             n2 = self.gru16(att[2], n2, inp[2], pool2x(n1))
@@ -507,16 +550,16 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 enc = disp.new_empty(B, nc + 1, H, W)
             fork = _side_stream(dev, 1) if MOTION_FORK else None
             if fork is not None:
-                fork.wait_stream(main)                   # forked from the origin (capture_fork)
+                stream_wait(fork, main)                   # forked from the origin (capture_fork)
             if MOTION_ON_MAIN:
                 self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
             else:
-                s_mot.wait_stream(main)
+                stream_wait(s_mot, main)
                 with torch.cuda.stream(s_mot):
                     self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
-            main.wait_stream(s_gru)                      # gru08(t): enqueued last on s_gru so far
+            stream_wait(main, s_gru)                      # gru08(t): enqueued last on s_gru so far
             if not MOTION_ON_MAIN:
-                main.wait_stream(s_mot)                  # motion(t)
+                stream_wait(main, s_mot)                  # motion(t)
             if t + 1 < iters:
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru16(t+1), beside gru04(t)
@@ -540,10 +583,10 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                     n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
                 _BRANCH[0] = 1
                 if not MOTION_ON_MAIN:
-                    main.wait_stream(s_mot)
+                    stream_wait(main, s_mot)
                 continue
             if t + 1 < iters:
-                s_gru.wait_stream(main)                  # gru04(t)
+                stream_wait(s_gru, main)                  # gru04(t)
                 # gru08's branches in order on the pipeline stream: a fork from it would be a side
                 # stream waiting on the pipeline stream and waited on by it (capture_fork)
                 _BRANCH[0] = 0
@@ -553,7 +596,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             if t + 1 == iters:
                 # test mode upsamples only the last iteration's disparity: the reference computes the
                 # mask head every iteration and discards all but the last (core/foundation_stereo.py:243-244)
-                s_mot.wait_stream(main)
+                stream_wait(s_mot, main)
                 with torch.cuda.stream(s_mot):
                     mask = _conv(self.mask[2], [_conv(self.mask[0], [n0], "relu")], "relu", alpha=0.25)
             if t + 1 < iters and HEAD_INPLACE:
@@ -565,10 +608,10 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             else:
                 disp = disp + self.disp_head(n0).float()
             if not MOTION_ON_MAIN or t + 1 == iters:
-                main.wait_stream(s_mot)
+                stream_wait(main, s_mot)
             if fork is not None:
-                main.wait_stream(fork)
-        main.wait_stream(s_gru)
+                stream_wait(main, fork)
+        stream_wait(main, s_gru)
         return [n0, n1, n2], mask, disp
 
     def _forward_fast(self, net, inp, corr, disp, att):

@@ -37,6 +37,13 @@ def test_gpus_n_spawns_n_ranks(n):
     B = 2 * n
     assert d["parity"]["pairs_checked"] == [0, B - 1]
     assert d["parity"]["max_abs_dd_px"] == 0.0 and d["parity"]["ok"] is True
+    # the attribution a multi-GPU line carries: every rank's step time and phase split, the world
+    # size each rank's process group reported
+    assert d["ranks"] == list(range(n)) and d["rank_world_size"] == [n] * n
+    for k in ("per_rank_ms", "scatter_ms", "run_ms", "allgather_ms"):
+        assert len(d[k]) == n and all(v >= 0.0 for v in d[k]), (k, d[k])
+    assert all(s + r + g <= p * 1.5 + 1.0 for s, r, g, p in zip(d["scatter_ms"], d["run_ms"], d["allgather_ms"],
+                                                                 d["per_rank_ms"]))
 
 
 def test_gpus_1_single_process():
