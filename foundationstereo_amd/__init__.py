@@ -3,15 +3,15 @@
 Hand-written gfx950 HIP kernels (``csrc/``, C ABI in ``include/fsmi.h``,
 loaded via ctypes from ``_lib/libfsmi.so``) behind the reference's own module
 and function API (``submodule``, ``geometry``, ``update``, ``utils``,
-``foundation_stereo``).  See DESIGN.md.
+``foundation_stereo``, and the backbone ``backbone.Feature``).  See DESIGN.md.
 """
 import os as _os
 
 __version__ = "0.1.0"
 
-# MIOpen runs only the few convs left outside the HIP kernels (the context net's 7x7 s2 stem and
-# 4x4 s4 `down`, the spx ConvTranspose2d pair, CAM / SAM) and every conv of the torch fallback
-# paths.  Its exhaustive Find benchmarks naive kernels (seconds each) on first use; instead ship the
+# MIOpen runs only the few convs left outside the HIP kernels (the context net's 7x7 stride-1 `conv1`,
+# CAM's 1x1 and SAM's 7x7 convs; tools/torch_conv_census.py lists them) and every conv of the torch
+# fallback paths.  Its exhaustive Find benchmarks naive kernels (seconds each) on first use; instead ship the
 # find-db measured on MI355X for these layer shapes (tuning/miopen) and use
 # FAST mode: db hit -> tuned solver, miss -> immediate-mode heuristic, never a
 # search.  Both are only defaults; an explicit environment wins.

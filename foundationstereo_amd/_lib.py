@@ -59,9 +59,6 @@ SIGNATURES = {
     "fsmi_elementwise": [_P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _I, _P],
     "fsmi_xca": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "fsmi_edgenext_mlp": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "fsmi_stream_create_cumask": [_P, _I, _P],
-    "fsmi_stream_destroy": [_P],
-    "fsmi_gru_small": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_pool2x": [_P, _P, _I, _I, _I, _I, _P],
     "fsmi_conv2d_1in": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],

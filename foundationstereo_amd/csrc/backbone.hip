@@ -319,7 +319,9 @@ __global__ __launch_bounds__(256) void bicubic_kernel(const float* __restrict__ 
   const int ox = static_cast<int>(i % Wo);
   const int oy = static_cast<int>((i / Wo) % Ho);
   const long long p = i / (static_cast<long long>(Ho) * Wo);
-  const float fy = sh * (oy + 0.5f) - 0.5f, fx = sw * (ox + 0.5f) - 0.5f;
+  // one rounding (fma), as the reference's vectorised CPU kernel computes it: at source coordinates of
+  // a few hundred pixels one fp32 ulp of the coordinate moves the taps' weights by ~3e-5
+  const float fy = fmaf(sh, oy + 0.5f, -0.5f), fx = fmaf(sw, ox + 0.5f, -0.5f);
   const int iy = static_cast<int>(floorf(fy)), ix = static_cast<int>(floorf(fx));
   float wy[4], wx[4];
   cubic_w(fy - iy, wy);

@@ -149,8 +149,6 @@ void pw_tile(int cfg, HaloArgs& a);
 // depth-blocked (17, 1, 1) volume tile (cfg 30, conv_depth.hip)
 bool depth_conv_ok(const HaloArgs& a);
 int launch_depth(HaloArgs& a, hipStream_t s);
-bool depth3_conv_ok(const HaloArgs& a);
-int launch_depth3(HaloArgs& a, hipStream_t s);
 
 // tiles with an in-block K-group (kg = 2) instantiation: the register-weight tiles that fit two
 // waves per SIMD (<= 256 VGPRs) with 512-thread blocks

@@ -195,19 +195,6 @@ int run_halo(HaloArgs& a, const char* what, const float* const* seg_ptr, const i
     if (rc != FSMI_OK) return rc;
     return finish_launch(what);
   }
-  if (cfg == 31) {                                 // depth-blocked (3, 3, 3) tile (conv_depth.hip)
-    FSMI_CHECK_ARG(d3 && KS == 3 && KD == 3 && a.str == 1 && !a.up && D > 1, "%s: tile 31 takes (3, 3, 3) "
-                   "stride-1 volume convs", what);
-    a.nsplit = 1;
-    a.kpc = KD * a.CinP / HKC;
-    a.ws = nullptr;
-    a.ts = nullptr;
-    a.ovf = range_flag_device();
-    g_cfg_launches[31].fetch_add(1, std::memory_order_relaxed);
-    const int rc = halo::launch_depth3(a, s);
-    if (rc != FSMI_OK) return rc;
-    return finish_launch(what);
-  }
   // cfg 32 + c: register-weight tile c (2..9) of a 2D map with the pipelined staging (conv_halo.h,
   // conv_halo_pipe_kernel); the volume instantiation (safe range mode) keeps the plain tile
   if (cfg >= 32) {

@@ -309,222 +309,6 @@ __global__ __launch_bounds__(512) void edgenext_mlp_kernel(MlpArgs a) {
 }
 
 
-// ---------------------------------------------------------------- one-round tile (FSMI_MLP_PX=80)
-// The 64-pixel tile above needs 300 blocks at cfg2 (19200 pixels): one block per CU (139 KB of LDS),
-// so the launch runs in two rounds and the second (44 blocks) costs a whole block time.  This tile
-// covers 80 pixels in 16-pixel MFMA fragments (v_mfma_f32_16x16x32_f16) -- 240 blocks, one round
-// -- and keeps only half of the 4C hidden map in LDS at a time (133 KB): GEMM 1 -> GELU -> split ->
-// GEMM 2 per half, each half with its own exact block exponent; GEMM 2's accumulators are
-// rescaled by the exact power of two between the halves.  Wave w: hidden rows [32 w, +32) of each
-// half (2 row fragments x 5 pixel fragments) in GEMM 1, output rows [16 w, +16) x 80 px in GEMM 2,
-// so every W1 / W2 fragment is loaded by exactly one wave.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-constexpr int kM80PX = 80, kM80NJ = 5;
-
-__device__ __forceinline__ void mma16x3(f32x4& acc, const half8& ah, const half8& al, const half8& bh,
-                                        const half8& bl) {
-  if constexpr (FSMI_NPROD == 3) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
-  }
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
-}
-
-template <int C>
-__global__ __launch_bounds__(512) void edgenext_mlp80_kernel(MlpArgs a) {
-  FSMI_TIMELINE_CLOCK(a.clk);
-  constexpr int E = 4 * C, EH = E / 2, PX = kM80PX, NJ = kM80NJ;
-  constexpr int XR = C + 8, HR = EH + 8;           // padded LDS rows (halves)
-  constexpr int NKX = C / HKC, NKH = EH / HKC;     // 32-channel chunks of x / of a hidden half
-  static_assert(C == 128 && 32 * kMlpWaves == EH && 16 * kMlpWaves == C, "edgenext_mlp80: C = 128");
-  __shared__ __attribute__((aligned(16))) _Float16 xim[2 * PX * XR];   // x hi, x lo
-  __shared__ __attribute__((aligned(16))) _Float16 him[2 * PX * HR];   // hidden half hi, lo
-  __shared__ __attribute__((aligned(16))) float red[kMlpWaves];
-  __shared__ __attribute__((aligned(16))) float2 lsb1[E];
-  __shared__ __attribute__((aligned(16))) float2 lsb2[C];
-  __shared__ __attribute__((aligned(16))) float lg[C];
-  _Float16(*Xh)[XR] = reinterpret_cast<_Float16(*)[XR]>(xim);
-  _Float16(*Xl)[XR] = reinterpret_cast<_Float16(*)[XR]>(xim + PX * XR);
-  _Float16(*Hh)[HR] = reinterpret_cast<_Float16(*)[HR]>(him);
-  _Float16(*Hl)[HR] = reinterpret_cast<_Float16(*)[HR]>(him + PX * HR);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = lane & 15, kg = lane >> 4;         // fragment row / column, k group (16x16x32 layout)
-  const int b = blockIdx.x / a.tiles;
-  const int p0 = (blockIdx.x - b * a.tiles) * PX;
-  const int HW = a.HW;
-  mlp_stamp(a, 0);
-
-  half8 w1f[NKX][2][2];                            // [chunk][row fragment][hi, lo]
-  auto load_w1 = [&](int hf) FSMI_HALO_INL {
-#pragma unroll
-    for (int c = 0; c < NKX; ++c)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const size_t o = (static_cast<size_t>(c) * E + hf * EH + 32 * wave + 16 * i + q) * HKC + 8 * kg;
-        w1f[c][i][0] = *reinterpret_cast<const half8*>(a.w1h + o);
-        w1f[c][i][1] = *reinterpret_cast<const half8*>(a.w1l + o);
-      }
-  };
-  load_w1(0);
-  for (int e = tid; e < E; e += 512) lsb1[e] = a.sb1[e];
-  if (tid < C) {
-    lsb2[tid] = a.sb2[tid];
-    lg[tid] = a.gamma ? a.gamma[tid] : 1.f;
-  }
-
-  // ---- x tile -> scaled hi / lo [pixel][channel] image
-  constexpr int XTASK = PX * (C / 8), XT = (XTASK + 511) / 512;
-  f32x8 xv[XT];
-  float mx = 0.f;
-#pragma unroll
-  for (int u = 0; u < XT; ++u) {
-    const int task = u * 512 + tid, p = task % PX, g = task / PX;
-    const bool ok = task < XTASK && p0 + p < HW;
-    const float* src = a.x + (static_cast<size_t>(b) * C + min(8 * g, C - 8)) * HW + min(p0 + p, HW - 1);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const float v = src[static_cast<size_t>(t) * HW];
-      xv[u][t] = ok ? v : 0.f;
-      mx = fmaxf(mx, fabsf(xv[u][t]));
-    }
-  }
-  const int sx = __builtin_amdgcn_readfirstlane(chunk_exp(block_max8(mx, red, lane, wave)));
-  {
-    const float xs = exp2i(sx == kNoExp ? 0 : sx);
-#pragma unroll
-    for (int u = 0; u < XT; ++u) {
-      const int task = u * 512 + tid, p = task % PX, g = task / PX;
-      if (task >= XTASK) continue;
-      const f32x8 v = xv[u] * xs;
-      const half8 hi = __builtin_convertvector(v, half8);
-      *reinterpret_cast<half8*>(&Xh[p][8 * g]) = hi;
-      if constexpr (FSMI_NPROD == 3)
-        *reinterpret_cast<half8*>(&Xl[p][8 * g]) = __builtin_convertvector(v - __builtin_convertvector(hi, f32x8), half8);
-    }
-  }
-  __syncthreads();
-  mlp_stamp(a, 1);
-
-  const float xinv = exp2i(sx == kNoExp ? 0 : -sx);
-  f32x4 acc2[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int sh_prev = 0;                                 // exponent of the half(s) already in acc2
-  float rv[NJ][4];                                 // residuals of the epilogue, loaded under GEMM 2
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    // ---- GEMM 1 (this half): hidden rows [32 w, +32) x 80 px, K = C
-    f32x4 acc1[2][NJ];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < NKX; ++c) {
-      half8 bh[NJ], bl[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        bh[j] = *reinterpret_cast<const half8*>(&Xh[16 * j + q][c * HKC + 8 * kg]);
-        if constexpr (FSMI_NPROD == 3) bl[j] = *reinterpret_cast<const half8*>(&Xl[16 * j + q][c * HKC + 8 * kg]);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) mma16x3(acc1[i][j], w1f[c][i][0], w1f[c][i][1], bh[j], bl[j]);
-    }
-    if (hf == 0) load_w1(1);                       // the next half's W1 under this half's GELU
-    // this half's W2 fragments (output rows 16 w + q), issued before the GELU
-    half8 w2f[NKH][2];
-#pragma unroll
-    for (int c = 0; c < NKH; ++c) {
-      const size_t o = ((static_cast<size_t>(hf) * NKH + c) * C + 16 * wave + q) * HKC + 8 * kg;
-      w2f[c][0] = *reinterpret_cast<const half8*>(a.w2h + o);
-      w2f[c][1] = *reinterpret_cast<const half8*>(a.w2l + o);
-    }
-    mlp_stamp(a, 2 + 2 * hf);
-    // bias + GELU; element r of acc1[i][j]: hidden row hf * EH + 32 w + 16 i + 4 kg + r, pixel 16 j + q
-    float hm = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        const int row = hf * EH + 32 * wave + 16 * i + 4 * kg + r;
-        const float2 qa = lsb1[row], qb = lsb1[row + 1];
-        const f32x2 sc = {qa.x * xinv, qb.x * xinv}, bi = {qa.y, qb.y};
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const f32x2 h = gelu_erf_h2(fma2(f32x2{acc1[i][j][r], acc1[i][j][r + 1]}, sc, bi));
-          const bool ok = p0 + 16 * j + q < HW;    // tail pixels: no effect on the max
-          acc1[i][j][r] = ok ? h.x : 0.f;
-          acc1[i][j][r + 1] = ok ? h.y : 0.f;
-          hm = fmaxf(hm, fmaxf(fabsf(acc1[i][j][r]), fabsf(acc1[i][j][r + 1])));
-        }
-      }
-    // the barrier in block_max8 also retires every wave's GEMM 2 reads of the previous half
-    const int sh = __builtin_amdgcn_readfirstlane(chunk_exp(block_max8(hm, red, lane, wave)));
-    const int she = sh == kNoExp ? 0 : sh;
-    {
-      const float hs = exp2i(she);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const f32x4 v = acc1[i][j] * hs;
-          const half4 hi = __builtin_convertvector(v, half4);
-          const int row = 32 * wave + 16 * i + 4 * kg;
-          *reinterpret_cast<half4*>(&Hh[16 * j + q][row]) = hi;
-          if constexpr (FSMI_NPROD == 3)
-            *reinterpret_cast<half4*>(&Hl[16 * j + q][row]) = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), half4);
-        }
-    }
-    if (hf == 1) {
-      // the epilogue's residuals (rows 16 w + 4 kg + r, pixels 16 j + q), loaded under GEMM 2
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int px = min(p0 + 16 * j + q, HW - 1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          rv[j][r] = a.res[(static_cast<size_t>(b) * C + 16 * wave + 4 * kg + r) * HW + px];
-      }
-      // acc2 (half 0, units 2^sh_prev) -> this half's units 2^she: an exact power-of-two rescale
-      const float f = exp2i(she - sh_prev);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc2[j] *= f;
-    }
-    sh_prev = she;
-    __syncthreads();
-    mlp_stamp(a, 3 + 2 * hf);
-    // ---- GEMM 2 (this half): output rows [16 w, +16) x 80 px, K = EH
-#pragma unroll
-    for (int c = 0; c < NKH; ++c) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const half8 bh = *reinterpret_cast<const half8*>(&Hh[16 * j + q][c * HKC + 8 * kg]);
-        half8 bl = bh;
-        if constexpr (FSMI_NPROD == 3) bl = *reinterpret_cast<const half8*>(&Hl[16 * j + q][c * HKC + 8 * kg]);
-        mma16x3(acc2[j], w2f[c][0], w2f[c][1], bh, bl);
-      }
-    }
-  }
-  mlp_stamp(a, 6);
-  // epilogue: out = res + gamma * (v * 2^-wexp * 2^-sh + b2)
-  const float hinv = exp2i(-sh_prev);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int px = p0 + 16 * j + q;
-    if (px >= HW) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = 16 * wave + 4 * kg + r;
-      const float2 qq = lsb2[co];
-      const float v = acc2[j][r] * (qq.x * hinv) + qq.y;
-      a.out[(static_cast<size_t>(b) * C + co) * HW + px] = rv[j][r] + lg[co] * v;
-    }
-  }
-  mlp_stamp(a, 7);
-}
-
 }  // namespace
 }  // namespace fsmi
 
@@ -552,18 +336,11 @@ extern "C" int fsmi_edgenext_mlp(const float* x, const float* res, float* out, c
   a.gamma = gamma;
   a.B = B;
   a.HW = H * W;
-  // FSMI_MLP_PX=80: the one-round 80-pixel tile (edgenext_mlp80_kernel); default the 64-pixel tile
-  static const int px80 = [] {
-    const char* e = std::getenv("FSMI_MLP_PX");
-    return e && std::atoi(e) == 80;
-  }();
-  const int PX = px80 ? kM80PX : kMlpPX;
-  a.tiles = (a.HW + PX - 1) / PX;
+  a.tiles = (a.HW + kMlpPX - 1) / kMlpPX;
   a.ts = g_conv_ts;
   hipStream_t s = as_stream(stream);
   a.clk = clock_slot(FSMI_K_CONV2D, s, 8ll * B * a.tiles, "edgenext_mlp", true);
   LaunchTimer t(FSMI_K_CONV2D, s);
-  if (px80) hipLaunchKernelGGL(edgenext_mlp80_kernel<128>, dim3(static_cast<unsigned>(B * a.tiles)), dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(edgenext_mlp_kernel<128>, dim3(static_cast<unsigned>(B * a.tiles)), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(edgenext_mlp_kernel<128>, dim3(static_cast<unsigned>(B * a.tiles)), dim3(512), 0, s, a);
   return finish_launch("fsmi_edgenext_mlp");
 }

@@ -186,19 +186,6 @@ LaunchTimer::~LaunchTimer() {
 
 extern "C" {
 
-// A stream whose kernels may run only on the CUs set in mask (nwords 32-bit words; bit i = CU i in the
-// runtime's numbering): hipExtStreamCreateWithCUMask.  Released with fsmi_stream_destroy.
-int fsmi_stream_create_cumask(const unsigned* mask, int nwords, void** stream) {
-  FSMI_CHECK_ARG(mask && nwords > 0 && stream, "fsmi_stream_create_cumask: bad arguments");
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(nwords), mask);
-  *stream = s;
-  return e == hipSuccess ? FSMI_OK : static_cast<int>(e);
-}
-
-int fsmi_stream_destroy(void* stream) {
-  return stream ? static_cast<int>(hipStreamDestroy(static_cast<hipStream_t>(stream))) : FSMI_OK;
-}
 
 }  // extern "C"
 

@@ -65,10 +65,7 @@ CTX_OVERLAP = os.environ.get("FSMI_CTX_OVERLAP", "1") != "0"
 # range guard of the split-precision convs, enforced per eager forward (see forward); FSMI_RANGE_GUARD=0
 # leaves the flag to the caller (ops.check_range)
 RANGE_GUARD = os.environ.get("FSMI_RANGE_GUARD", "1") != "0"
-# the cost-volume build + all-pairs pyramid before the side streams fork and the volume pyramid
-# before the classifier, each alone on the chip (FSMI_GEO_ALONE=0: the round-4 schedule, all-pairs +
-# volume pyramid on side stream 1 beside the classifier; for A/B)
-GEO_ALONE = os.environ.get("FSMI_GEO_ALONE", "1") != "0"
+
 
 
 def _gated(seq, x, gate):
@@ -347,7 +344,10 @@ class FoundationStereo(nn.Module):
             ctx_s = None
             ctx_overlap = _update.OVERLAP and CTX_OVERLAP and image1.is_cuda and not torch.is_grad_enabled()
             corr_pyr = None
-            geo_alone = ctx_overlap and GEO_ALONE
+            # the cost-volume build and the all-pairs correlation pyramid run ALONE on the chip, before any
+            # side stream forks (the volume pyramid follows the hourglass on the main stream, before the
+            # classifier): the north star's two HBM / MFMA kernels measured without co-running convs
+            geo_alone = ctx_overlap
             if geo_alone:
                 # the two HBM / MFMA kernels the north star measures run ALONE on the chip, before any
                 # side stream forks: the cost-volume build, then the all-pairs correlation pyramid (it
@@ -395,14 +395,7 @@ class FoundationStereo(nn.Module):
             else:
                 vol = self.corr_feature_att(self.corr_stem[1:](vol), features_left[0])
             vol = self.cost_agg(vol, features_left, gates=None if gates is None else gates[1:])
-            geo_fn = geo_s = None
-            if ctx_s is not None and not geo_alone:
-                # round-4 schedule (A/B): the geometry pyramids beside the classifier on side stream 1
-                geo_s = _update._side_stream(image1.device, 1)
-                stream_wait(geo_s, main)
-                with torch.cuda.stream(geo_s):
-                    geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(),
-                                                          vol.float(), num_levels=self.args.corr_levels, dx=self.dx)
+            geo_fn = None
             if corr_pyr is not None:
                 # the volume pyramid (HBM-bound) on the main stream right after the hourglass, before the
                 # classifier's convs start: the gate and disparity-transformer branches joined inside the
@@ -424,10 +417,6 @@ class FoundationStereo(nn.Module):
         if geo_fn is None:
             geo_fn = Combined_Geo_Encoding_Volume(features_left[0].float(), features_right[0].float(), vol.float(),
                                                   num_levels=self.args.corr_levels, dx=self.dx)
-        elif geo_s is not None:
-            stream_wait(main, geo_s)
-            for t in [*geo_fn.init_corr_pyramid, *geo_fn.geo_volume_pyramid]:
-                t.record_stream(main)
         disp = init_disp.float()
         disp_preds = []
         disp_up = None

@@ -410,10 +410,7 @@ def conv3d(x: Tensor, pk, bias: Tensor = None, act=None, res: Tensor = None, res
         _CONV_FLOPS["flops"] += 2 * Cin * pk.cout * pk.kd * pk.k * pk.k * B * Do * Ho * Wo
     stream = _stream(x)
     ws = _split_workspace(x.device, stream, 8 * B * pk.cout * Do * Ho * Wo)
-    auto = cfg < 0
     cfg, nsplit = _tuned(pk.k if stride == 1 else f"{pk.k}s2", pk.kd, Cin, pk.cout, B, D, H, W, cfg, nsplit)
-    if auto and _DEPTH3_TILE and stride == 1 and pk.k == 3 and pk.kd == 3 and Cin <= 32 and D > 1:
-        cfg, nsplit = 31, 1            # the rolled depth-blocked 3^3 walk (one 32-channel chunk)
     if cfg == 30 and not _DEPTH_TILE:
         cfg, nsplit = -1, -1           # A/B: the generic volume tiles (the C side picks)
     _lib.check(_lib.load().fsmi_conv3d_halo_x3_ex(
@@ -612,9 +609,6 @@ _SPLIT_CAP = int(os.environ.get("FSMI_SPLIT_CAP", "2"))
 # (17, 1, 1) volume convs (Conv3dNormActReduced.conv2) on the depth-blocked tile (cfg 30); 0: the
 # generic volume tiles from the tuning table (A/B)
 _DEPTH_TILE = os.environ.get("FSMI_DEPTH_TILE", "1") != "0"
-# (3, 3, 3) stride-1 volume convs of at most 32 input channels (corr_stem, the classifier) on the
-# rolled depth-blocked 3^3 tile (cfg 31) instead of the table's generic volume tile; 0: the table
-_DEPTH3_TILE = os.environ.get("FSMI_DEPTH3_TILE", "0") != "0"
 
 
 _SPLIT_WS = {}
@@ -712,37 +706,6 @@ def edgenext_mlp(x: Tensor, res: Tensor, pk1: "PackedConv", bias1: Tensor, pk2: 
                                              pk1.cout, H, W, _stream(x)), "edgenext_mlp")
     if _CONV_FLOPS["on"]:
         _CONV_FLOPS["flops"] += 2 * 2 * C * pk1.cout * B * H * W
-    return out
-
-
-def gru_small(hx: Tensor, xc: Tensor, h: Tensor, att: Tensor, pk_zr: "PackedConv", bias_zr: Tensor,
-              pk_q: "PackedConv", bias_q: Tensor, out: Tensor = None) -> Tensor:
-    """SelectiveConvGRU's small (1x1) RaftConvGRU branch weighted by ``att`` in one kernel
-    (core/update.py:83-95,117): ``((1 - z) h + z tanh(convq([r*h, xc]))) * att`` with
-    ``z, r = sigmoid(convz(hx)), sigmoid(convr(hx))``.  ``pk_zr``: PackedConv of [convz; convr]
-    (2Hd x K, 1x1); ``pk_q``: convq's (Hd x K, input channels [r*h, xc])."""
-    _check("gru_small", hx, xc, h, att, bias_zr, bias_q)
-    B, K, H, W = hx.shape
-    Hd = h.shape[1]
-    assert tuple(xc.shape) == (B, K - Hd, H, W) and tuple(h.shape) == (B, Hd, H, W) and \
-        tuple(att.shape) == (B, 1, H, W), \
-        f"gru_small: hx {tuple(hx.shape)}, xc {tuple(xc.shape)}, h {tuple(h.shape)}, att {tuple(att.shape)}"
-    assert pk_zr.k == 1 and pk_q.k == 1 and pk_zr.cin == K and pk_zr.cout == 2 * Hd and pk_q.cin == K and \
-        pk_q.cout == Hd, f"gru_small: zr {pk_zr.cout}x{pk_zr.cin}, q {pk_q.cout}x{pk_q.cin} for K={K}, Hd={Hd}"
-    hx, xc, h, att = _c(hx), _c(xc), _c(h), _c(att)
-    if out is None:
-        out = torch.empty_like(h)
-    else:
-        _check("gru_small", out)
-        if tuple(out.shape) != tuple(h.shape) or not out.is_contiguous():
-            raise RuntimeError(f"gru_small: out must be a contiguous {tuple(h.shape)} fp32 tensor")
-        if any(_overlaps(out, t) for t in (hx, xc, h, att)):
-            raise RuntimeError("gru_small: out must not alias an input")
-    _lib.check(_lib.load().fsmi_gru_small(
-        _p(hx), _p(xc), _p(h), _p(att), _p(out), _p(pk_zr.whi), _p(pk_zr.wlo), _p(pk_zr.scale_bias(bias_zr)),
-        _p(pk_q.whi), _p(pk_q.wlo), _p(pk_q.scale_bias(bias_q)), B, K, Hd, H, W, _stream(hx)), "gru_small")
-    if _CONV_FLOPS["on"]:
-        _CONV_FLOPS["flops"] += 2 * K * 3 * Hd * B * H * W
     return out
 
 

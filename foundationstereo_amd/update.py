@@ -35,12 +35,6 @@ FUSED_GATES = os.environ.get("FSMI_FUSED_GATES", "1") != "0"
 # PIPE_BRANCH: gru04's small branch on its own stream there
 PIPELINE = os.environ.get("FSMI_PIPELINE", "1") != "0"
 PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
-# run_pipelined: the disparity head of iteration t enqueued (captured) BEFORE gru08(t+1), which then
-# waits on an event recorded after gru04(t) instead of on the whole main stream (A/B knob)
-HEAD_FIRST = os.environ.get("FSMI_HEAD_FIRST", "0") != "0"
-# run_pipelined: the motion encoder's disparity branch (convd1, convd2) on the branch stream, beside the
-# lookup and convc1 / convc2 (A/B knob)
-MOTION_FORK = os.environ.get("FSMI_MOTION_FORK", "0") != "0"
 # run_pipelined: the motion path (lookup + encoder) on the main stream -- it is on the iteration's
 # critical chain between head(t-1) and gru04(t), both on main, with nothing beside it on main -- instead
 # of the motion stream (two cross-stream edges per iteration on that chain); A/B knob
@@ -145,9 +139,18 @@ def capture_fork_check(waiter, waited, capturing: bool, side_ids=None):
     _CAPTURE_EDGES.setdefault(a, set()).add(b)
 
 
+# diagnostics (tools/replay_timeline.py): while a list, every wait issued during a capture is logged as
+# (waiter stream handle, waited stream handle, number of clocked launches captured so far), which with
+# the capture-ordered clock records gives the captured graph's cross-stream edges
+WAIT_LOG = None
+
+
 def stream_wait(waiter, waited):
     """``waiter.wait_stream(waited)`` with the capture_fork check while a capture is in progress."""
-    capture_fork_check(waiter, waited, torch.cuda.is_current_stream_capturing())
+    capturing = torch.cuda.is_current_stream_capturing()
+    capture_fork_check(waiter, waited, capturing)
+    if WAIT_LOG is not None and capturing:
+        WAIT_LOG.append((waiter.cuda_stream, waited.cuda_stream, len(ops.timer_dump_captured())))
     waiter.wait_stream(waited)
 
 
@@ -159,15 +162,6 @@ _BRANCH = [1]
 EARLY_INTERP = os.environ.get("FSMI_EARLY_INTERP", "1") != "0"
 # DispHead's EdgeNeXt MLPs as one fused kernel (ops.edgenext_mlp); FSMI_FUSED_MLP=0: the two 1x1 convs
 _FUSED_MLP = os.environ.get("FSMI_FUSED_MLP", "1") != "0"
-# SelectiveConvGRU's small (1x1) branch as one fused kernel (ops.gru_small, opt-in: FSMI_GRU_SMALL=1); default:
-# the zr gate conv + the convq blend conv.  Alone the fused kernel is faster at every level (cfg2: 97 vs
-# 124, 41 vs 52, 27 vs 101 us at 1/4, 1/8, 1/16, tools/gru_small_bench.py), in the step slower (20.53-20.72
-# vs 20.74-21.00 pairs/s, any subset of levels): its 103-136 KB-LDS blocks wait for a drained CU beside the
-# other streams' conv blocks
-_GRU_SMALL = os.environ.get("FSMI_GRU_SMALL", "0") != "0"
-# ... on maps of at most / at least this many pixels per image (0: any)
-_GRU_SMALL_MAXPIX = int(os.environ.get("FSMI_GRU_SMALL_MAXPIX", "0"))
-_GRU_SMALL_MINPIX = int(os.environ.get("FSMI_GRU_SMALL_MINPIX", "0"))
 
 
 def _branch_stream(device):
@@ -255,20 +249,9 @@ class BasicMotionEncoder(nn.Module):
         """Writes cat([relu(conv(...)), disp]) into ``out`` (B, 128, H, W) without the cat copy."""
         return self._encode_rest(disp, _conv(self.convc1, [corr], "relu"), out)
 
-    def motion_into(self, disp, geo_fn, out, fork=None):
-        """The motion path of one iteration: the lookup ``geo_fn(disp)`` and this encoder.  ``fork``:
-        a stream the disparity branch (convd1, convd2 -- they read only ``disp``) runs on, beside the
-        lookup and the correlation branch.  The caller has made ``fork`` wait for ``disp`` (from the
-        capture's origin stream, see ``capture_fork``) and joins it later; its output is allocated
-        on the calling stream, which waits for ``fork`` before the last conv."""
-        if fork is None:
-            return self.encode_into(disp, geo_fn(disp), out)
-        B, _, H, W = disp.shape
-        d = disp.new_empty(B, self.convd2.out_channels, H, W)
-        with torch.cuda.stream(fork):
-            self._disp_feat(disp, d)
-        c1 = _conv(self.convc1, [geo_fn(disp)], "relu")
-        return self._encode_rest(disp, c1, out, d=d, join=fork)
+    def motion_into(self, disp, geo_fn, out):
+        """The motion path of one iteration: the lookup ``geo_fn(disp)`` and this encoder."""
+        return self.encode_into(disp, geo_fn(disp), out)
 
     def _disp_feat(self, disp, out=None):
         if _CONVD1_MIOPEN:                                     # A/B knob: the MIOpen conv + ReLU
@@ -277,12 +260,9 @@ class BasicMotionEncoder(nn.Module):
             d = ops.conv2d_1in(disp, self.convd1.weight, self.convd1.bias, relu=True)   # 7x7, 1 -> 64
         return _conv(self.convd2, [d], "relu", out=out)
 
-    def _encode_rest(self, disp, c1, out, d=None, join=None):
+    def _encode_rest(self, disp, c1, out):
         c = _conv(self.convc2, [c1], "relu")
-        if d is None:
-            d = self._disp_feat(disp)
-        if join is not None:
-            stream_wait(torch.cuda.current_stream(disp.device), join)
+        d = self._disp_feat(disp)
         # cat([cor, dsp]) with the disparity features (~disp magnitude: ~200 at cfg5) as the FIRST
         # segment: the halo conv fixes a block's exponent from its first chunk (conv_halo.h)
         nc, nd = c.shape[1], d.shape[1]
@@ -397,19 +377,10 @@ class SelectiveConvGRU(nn.Module):
                 return pk, b, z, rh
 
             sg = self.small_gru
-            fused_small = (_GRU_SMALL and sg.convq.kernel_size == (1, 1) and h.shape[1] == 128
-                           and hx.shape[1] in (384, 512) and xc.shape[1] == hx.shape[1] - 128
-                           and (not _GRU_SMALL_MAXPIX or h.shape[2] * h.shape[3] <= _GRU_SMALL_MAXPIX)
-                           and h.shape[2] * h.shape[3] >= _GRU_SMALL_MINPIX)
 
             def small():                                 # out = small branch * att
-                if fused_small:
-                    pkzr, bzr = _packed(sg.convz, sg.convr)
-                    pkq, bq = _packed(sg.convq)
-                    ops.gru_small(hx, xc, h, att, pkzr, bzr, pkq, bq, out=out)
-                else:
-                    pk, b, z, rh = branch(sg, "blend_small")
-                    ops.conv2d_gate([rh, xc], pk, b, "blend_small", h=h, z=z, att=att, out=out)
+                pk, b, z, rh = branch(sg, "blend_small")
+                ops.conv2d_gate([rh, xc], pk, b, "blend_small", h=h, z=z, att=att, out=out)
 
             if OVERLAP and _BRANCH[0]:
                 # small (1x1) branch on a side stream beside the large branch's zr conv; the
@@ -548,15 +519,12 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         for t in range(iters):
             if not HEAD_INPLACE and t:
                 enc = disp.new_empty(B, nc + 1, H, W)
-            fork = _side_stream(dev, 1) if MOTION_FORK else None
-            if fork is not None:
-                stream_wait(fork, main)                   # forked from the origin (capture_fork)
             if MOTION_ON_MAIN:
-                self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
+                self.encoder.motion_into(disp, geo_fn, enc)
             else:
                 stream_wait(s_mot, main)
                 with torch.cuda.stream(s_mot):
-                    self.encoder.motion_into(disp, geo_fn, enc, fork=fork)
+                    self.encoder.motion_into(disp, geo_fn, enc)
             stream_wait(main, s_gru)                      # gru08(t): enqueued last on s_gru so far
             if not MOTION_ON_MAIN:
                 stream_wait(main, s_mot)                  # motion(t)
@@ -571,20 +539,6 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
             _BRANCH[0] = 1 if main_branch else 0
             n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0))
             _BRANCH[0] = 1
-            if HEAD_FIRST and HEAD_INPLACE and t + 1 < iters:
-                ev04 = torch.cuda.Event()
-                ev04.record(main)                        # gru04(t) done: gru08(t+1) needs nothing else
-                enc = disp.new_empty(B, nc + 1, H, W)
-                self.disp_head(n0, res=disp, out=enc, co0=nc)
-                disp = enc[:, nc:]
-                s_gru.wait_event(ev04)
-                _BRANCH[0] = 0
-                with torch.cuda.stream(s_gru):           # gru08(t+1), beside the next motion path
-                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
-                _BRANCH[0] = 1
-                if not MOTION_ON_MAIN:
-                    stream_wait(main, s_mot)
-                continue
             if t + 1 < iters:
                 stream_wait(s_gru, main)                  # gru04(t)
                 # gru08's branches in order on the pipeline stream: a fork from it would be a side
@@ -609,8 +563,6 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 disp = disp + self.disp_head(n0).float()
             if not MOTION_ON_MAIN or t + 1 == iters:
                 stream_wait(main, s_mot)
-            if fork is not None:
-                stream_wait(main, fork)
         stream_wait(main, s_gru)
         return [n0, n1, n2], mask, disp
 

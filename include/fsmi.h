@@ -278,21 +278,6 @@ int fsmi_dwconv2d(const float* x, const float* w, const float* bias, float* out,
 int fsmi_edgenext_mlp(const float* x, const float* res, float* out, const void* w1hi, const void* w1lo,
                       const float* sb1, const void* w2hi, const void* w2lo, const float* sb2, const float* gamma,
                       int B, int C, int E, int H, int W, void* stream);
-/* fsmi_gru_small: SelectiveConvGRU's small (kernel 1) RaftConvGRU branch weighted by att
- *   (core/update.py:83-95,117; replaces the convz|convr gate conv + the convq blend conv):
- *   z = sigmoid(Wz hx + bz), r = sigmoid(Wr hx + br), q = tanh(Wq [r*h, xc] + bq),
- *   out = ((1 - z) h + z q) * att; hx (B,K,H,W) = conv1's output, xc (B,K-Hd,H,W) = conv0's output,
- *   h / out (B,Hd,H,W), att (B,1,H,W); wzhi/wzlo/sbz = ops.PackedConv of [convz; convr] (2Hd x K,
- *   1x1) and its (2^-wexp, bias) pairs, wqhi/wqlo/sbq = convq's (Hd x K, input order [r*h, xc]).
- *   Split-precision MFMA (3 fp16 products per MAC), fp32 accumulation and gates; z and r*h stay
- *   on chip.  Built for Hd = 128, K in {384, 512}; out must not alias an input. */
-int fsmi_gru_small(const float* hx, const float* xc, const float* h, const float* att, float* out,
-                   const void* wzhi, const void* wzlo, const float* sbz, const void* wqhi, const void* wqlo,
-                   const float* sbq, int B, int K, int Hd, int H, int W, void* stream);
-/* fsmi_stream_create_cumask: a HIP stream restricted to the CUs set in mask (nwords 32-bit words,
- *   hipExtStreamCreateWithCUMask); fsmi_stream_destroy releases it.  Diagnostics (tools/cumask_probe.py). */
-int fsmi_stream_create_cumask(const unsigned* mask, int nwords, void** stream);
-int fsmi_stream_destroy(void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
  *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */

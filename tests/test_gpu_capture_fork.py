@@ -2,17 +2,16 @@
 hipGraph with its optional stream forks, each in a child process (the knobs are read at import; a crash
 under capture must fail this test, not the runner):
 
-  * default: gru04's small branch and the motion encoder's disparity branch (convd1, convd2) on the
-    branch stream (FSMI_PIPE_BRANCH=1, FSMI_MOTION_FORK=1);
-  * FSMI_MOTION_FORK=0: the disparity branch back on the motion stream;
-  * everything in order on its stream (FSMI_PIPE_BRANCH=0, FSMI_MOTION_FORK=0);
-  * FSMI_MOTION_ON_MAIN=1: the motion path on the main stream (with and without the fork).
+  * default: gru04's small branch on the branch stream (FSMI_PIPE_BRANCH=1);
+  * everything in order on its stream (FSMI_PIPE_BRANCH=0);
+  * FSMI_MOTION_ON_MAIN=1: the motion path on the main stream.
 
 Every configuration runs the same kernels on the same inputs, so the eager forward and the replayed
 graph must be bit-identical across all of them.  faulthandler prints the Python stack of a segfault.
 Forking gru08's small branch from the pipeline stream (round 4's segfault) breaks the capture_fork rule
-(update.py): tools/capture_fork_probe.py reproduces that crash with plain torch ops; the last test here
-runs the probe's passing patterns."""
+(update.py): tools/capture_fork_probe.py reproduces that crash with plain torch ops; update.stream_wait
+now raises CaptureForkError before such a capture can end (tests/test_capture_fork_guard.py, and the
+last test here forces it under a real capture); the middle test runs the probe's passing patterns."""
 import json
 import os
 import subprocess
@@ -59,16 +58,14 @@ print(json.dumps({"finite": bool(np.isfinite(rep).all()), "mean": float(rep.mean
 
 CONFIGS = {
     "default": {},
-    "motion_fork": {"FSMI_MOTION_FORK": "1"},
-    "in_order": {"FSMI_PIPE_BRANCH": "0", "FSMI_MOTION_FORK": "0"},
+    "in_order": {"FSMI_PIPE_BRANCH": "0"},
     "motion_on_main": {"FSMI_MOTION_ON_MAIN": "1"},
-    "motion_on_main_fork": {"FSMI_MOTION_ON_MAIN": "1", "FSMI_MOTION_FORK": "1"},
 }
 
 
 def _run(name, tmp_path):
     env = dict(os.environ, REPO=REPO, OUT=str(tmp_path / name), **CONFIGS[name])
-    for k in ("FSMI_PIPE_BRANCH", "FSMI_MOTION_FORK", "FSMI_MOTION_ON_MAIN"):
+    for k in ("FSMI_PIPE_BRANCH", "FSMI_MOTION_ON_MAIN"):
         if k not in CONFIGS[name]:
             env.pop(k, None)
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
@@ -96,3 +93,29 @@ def test_capture_fork_rule_patterns():
         r = subprocess.run([sys.executable, "-c", probe.CHILD, v], capture_output=True, text=True, timeout=180)
         assert r.returncode == 0, f"{v}: exit {r.returncode}\n{r.stderr[-2000:]}"
         assert json.loads(r.stdout.strip().splitlines()[-1])["ok"], v
+
+
+@pytest.mark.gpu
+def test_guard_raises_under_real_capture():
+    """Forking gru08's small branch from the pipeline stream -- round 4's segfault -- raises
+    CaptureForkError inside the capture instead of reaching hipStreamEndCapture (child process)."""
+    code = CHILD.replace("with torch.cuda.graph(g):\n        out = model(L, R, iters=iters, test_mode=True)",
+                         "from foundationstereo_amd import update as U\n"
+                         "    real = U.SelectiveConvGRU.forward\n"
+                         "    def fwd(self, *a, **k):\n"
+                         "        U._BRANCH[0] = 1\n"
+                         "        return real(self, *a, **k)\n"
+                         "    U.SelectiveConvGRU.forward = fwd\n"
+                         "    try:\n"
+                         "        with torch.cuda.graph(g):\n"
+                         "            out = model(L, R, iters=iters, test_mode=True)\n"
+                         "    except Exception as e:\n"
+                         "        c, found = e, False\n"
+                         "        while c is not None:\n"
+                         "            found, c = found or isinstance(c, U.CaptureForkError), c.__context__\n"
+                         "        print(json.dumps({'raised': found})); sys.exit(0)\n"
+                         "    print(json.dumps({'raised': None})); sys.exit(0)")
+    env = dict(os.environ, REPO=REPO, OUT="/tmp/fsmi_guard")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"exit {r.returncode}\n{r.stderr[-3000:]}"
+    assert json.loads(r.stdout.strip().splitlines()[-1])["raised"], r.stdout[-500:]

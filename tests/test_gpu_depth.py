@@ -115,61 +115,3 @@ def test_product_selects_depth_tile(ops_mod, cin, D, H, W, name):
     assert counts[30] == 1 and sum(counts) == 1, [(i, c) for i, c in enumerate(counts) if c]
     generic = ops_mod.conv3d(g(x), pk, bias=g(bias), act="relu", cfg=7, nsplit=1)
     close(out, generic, atol=2e-5, rtol=1e-5)
-
-
-# ---------------------------------------------------------------- (3, 3, 3): cfg 31
-
-@pytest.mark.parametrize("act,res", [("leaky", None), ("relu", "pre"), (None, None), ("leaky", "post")])
-@pytest.mark.parametrize("cin,cout,D,H,W,B", [(28, 28, 48, 6, 40, 1), (28, 14, 20, 9, 33, 1), (14, 14, 7, 5, 20, 2),
-                                              (40, 37, 5, 7, 70, 1), (28, 28, 2, 3, 31, 1), (56, 56, 17, 4, 35, 1)])
-def test_depth3_conv_vs_torch(ops_mod, cin, cout, D, H, W, B, act, res):
-    """The depth-blocked 3^3 tile (cfg 31: each staged plane feeds up to three output depths over the
-    9 spatial taps, weights resident in LDS) vs fp64 torch: the stem's 28 channels, the classifier's
-    28 -> 14 / 14 -> 14, ragged channels (two chunks, two cout tiles) / rows / columns, volumes
-    shallower than the 16-deep tile, batch 2, the ResNet tail act(conv + res) and a post residual."""
-    gen = torch.Generator().manual_seed(cin * 7 + D)
-    x = torch.randn(B, cin, D, H, W, generator=gen)
-    w = torch.randn(cout, cin, 3, 3, 3, generator=gen) * 0.08
-    bias = torch.randn(cout, generator=gen) * 0.1
-    r = torch.randn(B, cout, D, H, W, generator=gen) if res else None
-    pk = ops_mod.PackedConv(g(w), mode="halo")
-    before = ops_mod.conv_launch_counts()[31]
-    out = ops_mod.conv3d(g(x), pk, bias=g(bias), act=act, res=g(r) if res else None, res_pre=res == "pre", cfg=31)
-    assert ops_mod.conv_launch_counts()[31] == before + 1
-    ref = F.conv3d(x.double(), w.double(), bias.double(), padding=1)
-    if res == "pre":
-        ref = ref + r.double()
-    ref = {"relu": F.relu, "leaky": lambda v: F.leaky_relu(v, 0.01), None: lambda v: v}[act](ref)
-    if res == "post":
-        ref = ref + r.double()
-    close(out, ref)
-
-
-def test_depth3_conv_feature_gate(ops_mod):
-    """FeatureAtt's sigmoid gate in the 3^3 tile's epilogue (corr_feature_att / the hourglass gates)."""
-    gen = torch.Generator().manual_seed(91)
-    B, cin, cout, D, H, W = 1, 28, 28, 24, 6, 40
-    x = torch.randn(B, cin, D, H, W, generator=gen)
-    w = torch.randn(cout, cin, 3, 3, 3, generator=gen) * 0.08
-    bias = torch.randn(cout, generator=gen) * 0.1
-    fatt = torch.randn(B, cout, H, W, generator=gen)
-    pk = ops_mod.PackedConv(g(w), mode="halo")
-    out = ops_mod.conv3d(g(x), pk, bias=g(bias), act="leaky", fatt=g(fatt), cfg=31)
-    ref = F.leaky_relu(F.conv3d(x.double(), w.double(), bias.double(), padding=1), 0.01) * \
-        torch.sigmoid(fatt.double())[:, :, None]
-    close(out, ref)
-
-
-def test_depth3_auto_knob(ops_mod, monkeypatch):
-    """FSMI_DEPTH3_TILE: auto-chosen (3, 3, 3) stride-1 convs of <= 32 input channels run the rolled
-    3^3 walk (cfg 31); wider inputs keep the table's tile."""
-    monkeypatch.setattr(ops_mod, "_DEPTH3_TILE", True)
-    gen = torch.Generator().manual_seed(93)
-    for cin, want in ((28, 1), (40, 0)):
-        x = torch.randn(1, cin, 13, 6, 40, generator=gen)
-        w = torch.randn(28, cin, 3, 3, 3, generator=gen) * 0.08
-        pk = ops_mod.PackedConv(g(w), mode="halo")
-        before = ops_mod.conv_launch_counts()[31]
-        out = ops_mod.conv3d(g(x), pk, act="leaky")
-        assert ops_mod.conv_launch_counts()[31] - before == want
-        close(out, F.leaky_relu(F.conv3d(x.double(), w.double(), padding=1), 0.01))

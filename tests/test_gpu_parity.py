@@ -845,70 +845,6 @@ def test_selective_gru_fused_vs_oracle(ops_mod, HW):
     close(out, ref, atol=2e-5)
 
 
-@pytest.mark.parametrize("K,HW,B", [(512, (24, 40), 1), (384, (13, 21), 2), (512, (60, 80), 1), (384, (30, 40), 1)])
-def test_gru_small_vs_torch(ops_mod, K, HW, B):
-    """ops.gru_small (the fused 1x1 SelectiveConvGRU branch, csrc/gru_small.hip) vs fp64 torch:
-    ((1 - z) h + z tanh(convq([sigmoid(convr hx) * h, x]))) * att, z = sigmoid(convz hx)
-    (core/update.py:83-95,117); ragged maps (13x21, 30x40) end in a partial 64-pixel tile."""
-    from foundationstereo_amd.update import RaftConvGRU, _packed
-    H, W = HW
-    Hd = 128
-    gru = RaftConvGRU(Hd, K - Hd, 1)
-    synth.init_module_(gru, seed=431 + K)
-    gru = gru.to(DEV).eval()
-    hx = np.abs(synth.normal(432, (B, K, H, W), 1.5))           # a ReLU output
-    xc = np.abs(synth.normal(433, (B, K - Hd, H, W)))
-    h = synth.normal(434, (B, Hd, H, W))
-    att = synth.uniform(435, (B, 1, H, W), 0.0, 1.0)
-    pkzr, bzr = _packed(gru.convz, gru.convr)
-    pkq, bq = _packed(gru.convq)
-    with torch.no_grad():
-        out = ops_mod.gru_small(g(hx), g(xc), g(h), g(att), pkzr, bzr, pkq, bq)
-    d = lambda a: torch.from_numpy(np.asarray(a)).double()        # noqa: E731
-    w = {k: v.detach().double().cpu() for k, v in gru.state_dict().items()}
-    z = torch.sigmoid(F.conv2d(d(hx), w["convz.weight"], w["convz.bias"]))
-    r = torch.sigmoid(F.conv2d(d(hx), w["convr.weight"], w["convr.bias"]))
-    q = torch.tanh(F.conv2d(torch.cat([r * d(h), d(xc)], 1), w["convq.weight"], w["convq.bias"]))
-    ref = ((1 - z) * d(h) + z * q) * d(att)
-    close(out, ref.float(), atol=2e-5)
-
-
-def test_gru_small_rejects_aliasing(ops_mod):
-    from foundationstereo_amd.update import RaftConvGRU, _packed
-    gru = RaftConvGRU(128, 256, 1).to(DEV).eval()
-    hx, xc = g(np.abs(synth.normal(441, (1, 384, 8, 8)))), g(synth.normal(442, (1, 256, 8, 8)))
-    h, att = g(synth.normal(443, (1, 128, 8, 8))), g(synth.uniform(444, (1, 1, 8, 8)))
-    pkzr, bzr = _packed(gru.convz, gru.convr)
-    pkq, bq = _packed(gru.convq)
-    with pytest.raises(RuntimeError, match="alias"):
-        ops_mod.gru_small(hx, xc, h, att, pkzr, bzr, pkq, bq, out=h)
-
-
-@pytest.mark.parametrize("HW", [(24, 40), (13, 21)])
-def test_selective_gru_small_fused_vs_oracle(ops_mod, HW, monkeypatch):
-    """SelectiveConvGRU at hidden 128 (the model's width): the small branch runs on the fused kernel
-    (no blend_small conv launched), the large one on the gate-epilogue convs, vs the oracle."""
-    from foundationstereo_amd import update as U
-    H, W = HW
-    B, Hd, Ci = 1, 128, 256
-    mod = U.SelectiveConvGRU(Hd, Ci + 128)
-    synth.init_module_(mod, seed=451)
-    mod = mod.to(DEV).eval()
-    h = synth.normal(452, (B, Hd, H, W))
-    x1, x2 = synth.normal(453, (B, Ci, H, W)), synth.normal(454, (B, 128, H, W))
-    att = synth.uniform(455, (B, 1, H, W), 0.0, 1.0)
-    monkeypatch.setattr(U, "_GRU_SMALL", True)                  # opt-in in the product (update.py)
-    modes = []
-    real = ops_mod.conv2d_gate
-    monkeypatch.setattr(ops_mod, "conv2d_gate", lambda *a, **k: (modes.append(a[3]), real(*a, **k))[1])
-    with torch.no_grad():
-        out = mod(g(att), g(h), g(x1), g(x2))
-    assert "blend_small" not in modes and modes.count("blend_large") == 1, modes
-    P = {"m." + k: v.cpu() for k, v in mod.state_dict().items()}
-    ref = oracle.stereo_oracle.selective_gru(P, "m", t(att), t(h), t(x1), t(x2))
-    close(out, ref, atol=2e-5)
-
-
 def test_update_step_golden(ops_mod):
     gd = load_golden("update_step")
     from foundationstereo_amd.update import BasicSelectiveMultiUpdateBlock

@@ -10,8 +10,12 @@ slows the step (~17 vs ~21 pairs/s at cfg2), so its per-iteration picture is not
 
 Prints, for iteration ``--iter`` (lookup(t) start .. lookup(t+1) start): every stamped launch with its
 capture stream (main / motion / branch / pipeline), start / end in us from lookup(t), duration and tag;
-the busy time per stream; and the chain that sets the iteration's length (from lookup(t+1) back, each
-step the launch that finished last before the current one started).  Kernels without a clock (the
+the busy time per stream; and the chain that sets the iteration's length, walked back from lookup(t+1)
+through the captured graph's dependencies: each launch's own-stream predecessor plus, for every
+cross-stream wait its stream issued (logged with its capture position, update.WAIT_LOG), the waited
+stream's last launch before the wait; each step takes the dependency that finished last.  (Round 5's
+tool took the latest-ending launch of ANY stream at each step, which walked into the pipeline stream
+whenever one of its convs happened to end just before a main-stream launch.)  Kernels without a clock (the
 few non-fsmi ops, MIOpen) are absent, so gaps in the chain can hide them.  Also the whole step: span,
 kernel time per stream and the sum over launches per tag family.
 """
@@ -58,9 +62,11 @@ with torch.no_grad():
         model(L, R, iters=iters, test_mode=True)
     torch.cuda.synchronize()
     ops.timer_enable(True, timeline=True)
+    fupdate.WAIT_LOG = []                    # the capture's cross-stream waits, by capture position
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         model(L, R, iters=iters, test_mode=True)
+    waits, fupdate.WAIT_LOG = fupdate.WAIT_LOG, None
     ops.timer_enable(False)
 for _ in range(a.replays):
     g.replay()
@@ -74,8 +80,25 @@ step_ms = e0.elapsed_time(e1)
 names = {}
 for idx, nm in ((0, "motion"), (1, "branch"), (3, "pipeline")):
     names[fupdate._side_stream(dev, idx).cuda_stream] = nm
-recs = [{"k": k, "stream": names.get(sp, "main"), "s": t0, "e": t1, "tag": tag or _lib.KERNELS[k]}
-        for k, sp, t0, t1, tag in ops.timer_dump_captured()]
+recs = [{"k": k, "sp": sp, "stream": names.get(sp, "main"), "s": t0, "e": t1, "tag": tag or _lib.KERNELS[k], "i": i}
+        for i, (k, sp, t0, t1, tag) in enumerate(ops.timer_dump_captured())]
+# the captured graph's dependencies of each launch (capture position i): its stream's previous launch,
+# and for every wait its stream issued since that launch (capture position <= i), the waited stream's
+# last launch captured before the wait
+by_pos = list(recs)
+last_on = {}
+deps = {}
+for r in by_pos:
+    prev = last_on.get(r["sp"])
+    d = [prev] if prev is not None else []
+    lo = prev["i"] if prev is not None else -1
+    for (ws, wd, k) in waits:
+        if ws == r["sp"] and lo < k <= r["i"]:
+            cand = [q for q in by_pos[:k] if q["sp"] == wd]
+            if cand:
+                d.append(cand[-1])
+    deps[r["i"]] = d
+    last_on[r["sp"]] = r
 recs = [r for r in recs if r["s"] and r["e"] >= r["s"]]
 recs.sort(key=lambda r: r["s"])
 out = []
@@ -125,7 +148,9 @@ if len(lk) > a.iter + 1:
     emit("  busy per stream: " + ", ".join(f"{k} {v / 100:.0f} us ({v / (t1 - t0):.0%})" for k, v in sorted(busy.items())))
     chain, cur = [nxt], nxt
     while True:
-        cands = [r for r in recs if r["e"] <= cur["s"] and r["e"] > t0 and r is not cur]
+        # the binding dependency: of the launch's graph dependencies (own-stream predecessor, waited-on
+        # streams' launches), the one that finished last
+        cands = [q for q in deps.get(cur["i"], []) if q["e"] > t0 and q["s"]]
         if not cands:
             break
         p = max(cands, key=lambda r: r["e"])
@@ -135,8 +160,9 @@ if len(lk) > a.iter + 1:
         cur = p
     chain.reverse()
     ktime = sum(r["e"] - r["s"] for r in chain if r["s"] >= t0 and r is not nxt)
-    emit(f"  critical chain: {len(chain)} launches, {ktime / 100:.0f} us of kernels + "
-         f"{(t1 - t0 - ktime) / 100:.0f} us between them (gaps, unstamped kernels)")
+    emit(f"  critical chain (from the captured graph's edges: own-stream order + the logged cross-stream waits; "
+         f"each step back the dependency that finished last): {len(chain)} launches, {ktime / 100:.0f} us of "
+         f"kernels + {(t1 - t0 - ktime) / 100:.0f} us between them (launch gaps, unstamped kernels)")
     for r in chain:
         emit(f"    {r['stream']:>8} {(r['s'] - t0) / 100:8.1f} {(r['e'] - t0) / 100:8.1f} {(r['e'] - r['s']) / 100:7.1f}  {r['tag']}")
 if a.list:
