@@ -482,6 +482,9 @@ def main():
         "output_finite": out_finite,
         # forwards re-run in safe range mode after their range flag came back set (ops.guarded)
         "range_recoveries": ops.RANGE_RECOVERIES[0],
+        # HBM high-water mark of this rank's process (caching allocator: tensors, workspaces, the captured
+        # graph's private pool) -- the 288 GB budget the per-GPU batch is sized against
+        "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3),
         "config": {"workload": f"{a.config}: {W}x{H}{' hierarchical' if a.config in HIERA else ''}, "
                                f"max_disp {md}, {iters} iters, {vit}, "
                                f"corr_levels {L}, {per_gpu} pair(s)/GPU; forward "

@@ -53,8 +53,12 @@ bool take(int k, hipEvent_t* s, hipEvent_t* e) {
 }  // namespace
 
 // in-kernel clock: a device arena of per-wave (start, end) stamps, bump-allocated per launch and
-// zeroed at enable / reset; per kernel the host keeps (offset, nwaves) of each launch
-constexpr size_t kClockArena = size_t(1) << 26;       // u64 stamps (512 MB: a timeline of a whole forward)
+// zeroed at enable / reset; per kernel the host keeps (offset, nwaves) of each launch.  4M stamps (32 MB)
+// serve timer modes 1 / 2 (bench.py: only the geometry kernels stamp); timer mode 3 (the timeline
+// build's whole forward) grows it to 64M (512 MB) when no captured graph holds slots in it
+constexpr size_t kClockArenaSmall = size_t(1) << 22;
+constexpr size_t kClockArenaBig = size_t(1) << 26;
+size_t g_clock_cap = 0;                                // stamps allocated
 unsigned long long* g_clock = nullptr;
 size_t g_clock_top = 0;
 // slots handed to launches captured into a hipGraph (timer mode 2) stay reserved for the life of the
@@ -78,12 +82,21 @@ std::vector<CapRecord> g_clock_caplog;
 // launches that found the arena full, eager (this session) and captured (reported by the queries)
 long long g_clock_dropped[FSMI_K_COUNT], g_clock_dropped_cap[FSMI_K_COUNT];
 
-static int clock_init() {
-  if (!g_clock && hipMalloc(&g_clock, sizeof(unsigned long long) * kClockArena) != hipSuccess) {
+static int clock_init(bool big = false) {
+  const size_t want = big ? kClockArenaBig : kClockArenaSmall;
+  if (g_clock && g_clock_cap < want && g_clock_floor == 0) {   // grow: no graph holds a slot in it
+    if (hipDeviceSynchronize() != hipSuccess || hipFree(g_clock) != hipSuccess) return FSMI_ERR_ARG;
     g_clock = nullptr;
-    return FSMI_ERR_ARG;
   }
-  if (hipMemset(g_clock + g_clock_floor, 0, sizeof(unsigned long long) * (kClockArena - g_clock_floor)) !=
+  if (!g_clock) {
+    if (hipMalloc(&g_clock, sizeof(unsigned long long) * want) != hipSuccess) {
+      g_clock = nullptr;
+      g_clock_cap = 0;
+      return FSMI_ERR_ARG;
+    }
+    g_clock_cap = want;
+  }
+  if (hipMemset(g_clock + g_clock_floor, 0, sizeof(unsigned long long) * (g_clock_cap - g_clock_floor)) !=
       hipSuccess)
     return FSMI_ERR_ARG;
   g_clock_top = g_clock_floor;
@@ -102,7 +115,7 @@ unsigned long long* clock_slot(int kernel, hipStream_t stream, long long nwaves,
   std::lock_guard<std::mutex> lk(g_mu);
   const size_t need = 2 * static_cast<size_t>(nwaves);
   const bool captured = st != hipStreamCaptureStatusNone;
-  if (g_clock_top + need > kClockArena) {
+  if (g_clock_top + need > g_clock_cap) {
     // the query of this kernel fails instead of silently under-counting
     ++(captured ? g_clock_dropped_cap : g_clock_dropped)[kernel];
     return nullptr;
@@ -204,7 +217,7 @@ int fsmi_timer_enable(int on) {
   fsmi::g_timeline = on == 3;
   for (auto& f : fsmi::g_replay) f = nullptr;      // a replay only targets buffers of the current session
   if (fsmi::g_enabled) {
-    if (fsmi::clock_init() != FSMI_OK) {
+    if (fsmi::clock_init(fsmi::g_timeline) != FSMI_OK) {
       fsmi::set_error("fsmi_timer_enable: clock slots");
       return FSMI_ERR_ARG;
     }
@@ -228,7 +241,7 @@ int fsmi_timer_reset(void) {
   for (auto& p : fsmi::g_pool) p.used = 0;
   for (auto& f : fsmi::g_replay) f = nullptr;
   if (fsmi::g_enabled) {
-    if (hipDeviceSynchronize() != hipSuccess || fsmi::clock_init() != FSMI_OK) {
+    if (hipDeviceSynchronize() != hipSuccess || fsmi::clock_init(fsmi::g_timeline) != FSMI_OK) {
       fsmi::set_error("fsmi_timer_reset: clock slots");
       return FSMI_ERR_ARG;
     }
@@ -395,6 +408,15 @@ int fsmi_timer_release_captured(void) {
   for (auto& d : fsmi::g_clock_dropped_cap) d = 0;
   fsmi::g_clock_floor = 0;
   fsmi::g_clock_top = 0;
+  // the slots are handed out again from 0: start a clean session (the arena zeroed, this session's eager
+  // records -- which point into slots about to be reused -- and their drop counts cleared), so a later
+  // launch never reads another launch's stale stamps
+  if (fsmi::g_clock) {
+    if (hipDeviceSynchronize() != hipSuccess || fsmi::clock_init(fsmi::g_timeline) != FSMI_OK) {
+      fsmi::set_error("fsmi_timer_release_captured: clock slots");
+      return FSMI_ERR_ARG;
+    }
+  }
   return FSMI_OK;
 }
 

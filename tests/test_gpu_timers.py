@@ -57,5 +57,12 @@ def test_lookup_clock_in_captured_graph():
         del g
         ops.timer_release_captured()
         assert ops.timer_query_clock("lookup", captured=True)[1] == 0
+        # release starts a clean session (timing still on): the eager records are gone, and a new eager
+        # launch gets a zeroed slot -- a sane duration, not another launch's stale stamps
+        assert ops.timer_query_clock("lookup")[1] == 0
+        ops.geo_lookup(pyr, corr, disp, 4)
+        torch.cuda.synchronize()
+        ms, n = ops.timer_query_clock("lookup")
+        assert n == 1 and 0.0 < ms < 5.0, (ms, n)
     finally:
         ops.timer_enable(False)
