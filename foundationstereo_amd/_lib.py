@@ -50,7 +50,8 @@ SIGNATURES = {
     "fsmi_dwconv2d": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_dwconv2d_ex": [_P, _I, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_channel_layernorm": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
-    "fsmi_vit_attention": [_P, _P, _I, _I, _I, _I, _I, _F, _P],
+    "fsmi_vit_attention": [_P, _P, _I, _I, _I, _I, _I, _F, _P, ctypes.c_longlong, _P],
+    "fsmi_vit_attention_ws_floats": [_I, _I, _I, _I],
     "fsmi_space_to_depth": [_P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_depth_to_space": [_P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_vit_tokens": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
@@ -58,6 +59,7 @@ SIGNATURES = {
     "fsmi_instance_norm": [_P, _P, _P, _I, _I, _F, _I, _I, _P],
     "fsmi_elementwise": [_P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _I, _P],
     "fsmi_xca": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "fsmi_xca_workspace_floats": [_I, _I, _I],
     "fsmi_edgenext_mlp": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_pool2x": [_P, _P, _I, _I, _I, _I, _P],
@@ -80,6 +82,7 @@ SIGNATURES = {
     "fsmi_timer_query_clock_captured": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)],
     "fsmi_timer_release_captured": [],
     "fsmi_timer_dump_captured": [ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)],
+    "fsmi_timer_captured_count": [ctypes.POINTER(ctypes.c_longlong)],
 }
 
 KERNELS = ["gwc", "concat", "comb", "proj", "corr", "volpyr", "lookup", "sampler", "reg", "upsample",
@@ -126,7 +129,8 @@ def load():
         if fn is None:
             raise FsmiError(f"{path}: missing symbol {name}")
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_char_p if name in ("fsmi_last_error", "fsmi_arch") else ctypes.c_int
+        fn.restype = (ctypes.c_char_p if name in ("fsmi_last_error", "fsmi_arch") else
+                      ctypes.c_longlong if name.endswith("_floats") and name != "fsmi_dt_layer_floats" else ctypes.c_int)
     _lib = lib
     return lib
 

@@ -26,9 +26,12 @@ typedef float bf32x4 __attribute__((ext_vector_type(4)));
 // with the biased variance over the C channels of token t (nn.LayerNorm over the last dim of the
 // reference's token-major (B, T, C) tensors, dinov2 layers/block.py:63,75, vision_transformer.py:96;
 // LayerNorm2d / channels-last LayerNorm in EdgeNeXt).  Block = 16 tokens x 16 channel groups: lanes
-// over consecutive tokens read 64-B runs of each channel row; two passes over the column (mean, then
-// the centred variance) and the normalising pass re-read it from L2.
-constexpr int LN_TB = 16, LN_G = 16;
+// over consecutive tokens read 64-B runs of each channel row.  Each thread loads its C / 16 channel
+// values of its token ONCE into registers (all loads issued before the first use), so the mean, the
+// centred variance and the normalised output are computed from registers: one HBM read and one write
+// per element (round 6; the three-pass form re-read the column twice and waited one load latency per
+// channel: 13.8 us per ViT-S LayerNorm at cfg2).
+constexpr int LN_TB = 16, LN_G = 16, LN_MAXN = 64;          // C <= LN_G * LN_MAXN = 1024
 
 __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ x, float* __restrict__ out,
                                                       const float* __restrict__ w, const float* __restrict__ bias,
@@ -39,8 +42,13 @@ __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ 
   const int t = (blockIdx.x - b * ntiles) * LN_TB + tok;
   const bool valid = t < n;
   const float* xp = x + static_cast<size_t>(b) * C * Tx + min(t, n - 1);
+  const int cnt = (C - grp + LN_G - 1) / LN_G;              // channels grp, grp + 16, ...
+  float v[LN_MAXN];
   float s = 0.f;
-  for (int c = grp; c < C; c += LN_G) s += xp[static_cast<size_t>(c) * Tx];
+#pragma unroll
+  for (int k = 0; k < LN_MAXN; ++k) v[k] = k < cnt ? xp[static_cast<size_t>(grp + LN_G * k) * Tx] : 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXN; ++k) s += v[k];
   red[grp][tok] = s;
   __syncthreads();
   float tot = 0.f;
@@ -49,21 +57,25 @@ __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ 
   const float mean = tot / static_cast<float>(C);
   __syncthreads();
   float s2 = 0.f;
-  for (int c = grp; c < C; c += LN_G) {
-    const float d = xp[static_cast<size_t>(c) * Tx] - mean;
+#pragma unroll
+  for (int k = 0; k < LN_MAXN; ++k) {
+    const float d = k < cnt ? v[k] - mean : 0.f;
     s2 = fmaf(d, d, s2);
   }
   red[grp][tok] = s2;
   __syncthreads();
-  float v = 0.f;
+  float var = 0.f;
 #pragma unroll
-  for (int g = 0; g < LN_G; ++g) v += red[g][tok];
-  const float rstd = 1.f / sqrtf(v / static_cast<float>(C) + eps);
+  for (int g = 0; g < LN_G; ++g) var += red[g][tok];
+  const float rstd = 1.f / sqrtf(var / static_cast<float>(C) + eps);
   if (!valid) return;
   float* op = out + static_cast<size_t>(b) * C * To + t;
-  for (int c = grp; c < C; c += LN_G) {
-    const float y = (xp[static_cast<size_t>(c) * Tx] - mean) * rstd;
-    op[static_cast<size_t>(c) * To] = fmaf(y, w ? w[c] : 1.f, bias ? bias[c] : 0.f);
+#pragma unroll
+  for (int k = 0; k < LN_MAXN; ++k) {
+    if (k < cnt) {
+      const int c = grp + LN_G * k;
+      op[static_cast<size_t>(c) * To] = fmaf((v[k] - mean) * rstd, w ? w[c] : 1.f, bias ? bias[c] : 0.f);
+    }
   }
 }
 
@@ -85,6 +97,11 @@ __global__ __launch_bounds__(256) void chan_ln_kernel(const float* __restrict__ 
 //   accumulator layout dictates), scaled by 2^12 before its hi / lo split so small probabilities keep
 //   their low half normal; A = V from an LDS [d][key] image, read in the matching key order.
 // The next key block's K / V are loaded into registers before the current block's MFMAs.
+// Key split (round 6): B * heads * Tp / 32 query waves is below one wave per SIMD at ViT-S cfg2 (744
+// waves for 1024 SIMDs, every wave alone on its SIMD with nothing to hide its latencies: 78 us per
+// launch), so the key blocks are divided into nsplit ranges, one block per (image, head, 128
+// queries, range); each writes its unnormalised O^T with its running max m and sum l, and
+// vit_attn_combine_kernel merges the ranges (in range order) with the 2^(m_s - max m) weights.
 constexpr int ATT_HD = 64, ATT_KB = 64, ATT_KR = ATT_HD + 8, ATT_VR = ATT_KB + 4;
 constexpr float ATT_PSCALE = 4096.f;
 
@@ -97,13 +114,16 @@ __device__ __forceinline__ void mma3b(bf32x16& acc, const bhalf8& ah, const bhal
 
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                           int nh, int T, int Tp, float qscale, int nqt) {
+                                                           int nh, int T, int Tp, float qscale, int nqt, int nsplit,
+                                                           int kbs, float* __restrict__ opart,
+                                                           float* __restrict__ mlpart) {
   constexpr int NT = NW * 64, KT = ATT_KB * ATT_HD / 8 / NT, VT = ATT_KB * ATT_HD / 4 / NT;
   static_assert(KT >= 1 && VT >= 1, "vit_attn: block too large");
   __shared__ __attribute__((aligned(16))) _Float16 kt[2][ATT_KB][ATT_KR];   // [hi, lo][key][d]
   __shared__ __attribute__((aligned(16))) _Float16 vs[2][ATT_HD][ATT_VR];   // [hi, lo][d][key]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, r32 = lane & 31;
-  const int qt = blockIdx.x % nqt, bh = blockIdx.x / nqt;
+  const int sp = blockIdx.x % nsplit, qb = blockIdx.x / nsplit;
+  const int qt = qb % nqt, bh = qb / nqt;
   const int h = bh % nh, b = bh / nh;
   const size_t P = static_cast<size_t>(Tp);
   const float* Q = qkv + (static_cast<size_t>(b) * 3 * nh * ATT_HD + static_cast<size_t>(h) * ATT_HD) * P;
@@ -163,9 +183,9 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(const float* __restri
   bf32x16 o[2];
 #pragma unroll
   for (int r = 0; r < 16; ++r) o[0][r] = o[1][r] = 0.f;
-  const int nkb = (T + ATT_KB - 1) / ATT_KB;
-  gload(0);
-  for (int kb = 0; kb < nkb; ++kb) {
+  const int kb_begin = sp * kbs, nkb = min((T + ATT_KB - 1) / ATT_KB, kb_begin + kbs);
+  gload(kb_begin * ATT_KB);
+  for (int kb = kb_begin; kb < nkb; ++kb) {
     __syncthreads();                 // every wave is done reading the previous block's images
     lstore();
     __syncthreads();
@@ -235,15 +255,71 @@ __global__ __launch_bounds__(NW * 64) void vit_attn_kernel(const float* __restri
         }
       }
   }
-  const float inv = 1.f / (l * ATT_PSCALE);
   const int qo = q0 + r32;
   if (qo >= Tp) return;
+  if (nsplit > 1) {                // this key range's partial: O^T unnormalised, m, l
+    const int nbh = gridDim.x / (nsplit * nqt);                                     // B * nh
+    const size_t slot = static_cast<size_t>(sp) * nbh + bh;
+    float* op = opart + slot * ATT_HD * P + qo;
+#pragma unroll
+    for (int df = 0; df < 2; ++df)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) op[static_cast<size_t>(df * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * P] = o[df][r];
+    if (hh == 0) {
+      mlpart[slot * 2 * P + qo] = m;
+      mlpart[slot * 2 * P + P + qo] = l;
+    }
+    return;
+  }
+  const float inv = 1.f / (l * ATT_PSCALE);
   float* op = out + (static_cast<size_t>(b) * nh + h) * ATT_HD * P + qo;
 #pragma unroll
   for (int df = 0; df < 2; ++df)
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       op[static_cast<size_t>(df * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * P] = o[df][r] * inv;
+}
+
+// out[bh, d, q] = sum_s 2^(m_s - M) O_s[d, q] / (sum_s 2^(m_s - M) l_s * PSCALE), M = max_s m_s; one
+// thread per (bh, 8 channels, query)
+__global__ __launch_bounds__(256) void vit_attn_combine_kernel(const float* __restrict__ opart,
+                                                               const float* __restrict__ mlpart,
+                                                               float* __restrict__ out, int nbh, int Tp, int nsplit) {
+  const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const int q = static_cast<int>(i % Tp);
+  const long long r = i / Tp;
+  const int dg = static_cast<int>(r % (ATT_HD / 8));
+  const int bh = static_cast<int>(r / (ATT_HD / 8));
+  if (bh >= nbh) return;
+  const size_t P = static_cast<size_t>(Tp);
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, mlpart[(static_cast<size_t>(s) * nbh + bh) * 2 * P + q]);
+  float L = 0.f, acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const size_t slot = static_cast<size_t>(s) * nbh + bh;
+    const float w = __builtin_amdgcn_exp2f(mlpart[slot * 2 * P + q] - M);
+    L = fmaf(mlpart[slot * 2 * P + P + q], w, L);
+    const float* op = opart + (slot * ATT_HD + 8 * dg) * P + q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = fmaf(op[j * P], w, acc[j]);
+  }
+  const float inv = 1.f / (L * ATT_PSCALE);
+  float* o = out + (static_cast<size_t>(bh) * ATT_HD + 8 * dg) * P + q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j * P] = acc[j] * inv;
+}
+
+// key ranges per (image, head, 128-query tile): enough blocks for two per CU, >= 4 key blocks each
+int vit_attn_splits(int B, int heads, int T, int Tp, int* kbs) {
+  const int nkb = (T + ATT_KB - 1) / ATT_KB;
+  const long long nb = static_cast<long long>(B) * heads * ((Tp + 127) / 128);
+  int ns = static_cast<int>(std::min<long long>(8, (512 + nb - 1) / nb));
+  ns = std::max(1, std::min(ns, nkb / 4));
+  const int per = (nkb + ns - 1) / ns;
+  *kbs = per;
+  return (nkb + per - 1) / per;
 }
 
 // ---------------------------------------------------------------- layout kernels
@@ -361,26 +437,58 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
+// REG: planes of HW <= 256 * IN_MAXN are read once into registers (all loads in flight together) and
+// normalised from them -- one HBM read and one write per element; larger planes take three passes.
+constexpr int IN_MAXN = 80;               // 20480 px: a 1/4-resolution plane at 640x480
+
+template <bool REG>
 __global__ __launch_bounds__(256) void instnorm_kernel(const float* __restrict__ x, const float* __restrict__ res,
                                                        float* __restrict__ out, int HW, float eps, int act1,
                                                        int act2) {
   __shared__ float red[4];
   const float* xp = x + static_cast<size_t>(blockIdx.x) * HW;
-  float s = 0.f;
-  for (int i = threadIdx.x; i < HW; i += 256) s += xp[i];
-  const float mean = block_sum256(s, red) / static_cast<float>(HW);
-  float s2 = 0.f;
-  for (int i = threadIdx.x; i < HW; i += 256) {
-    const float d = xp[i] - mean;
-    s2 = fmaf(d, d, s2);
-  }
-  const float rstd = 1.f / sqrtf(block_sum256(s2, red) / static_cast<float>(HW) + eps);
   float* op = out + static_cast<size_t>(blockIdx.x) * HW;
   const float* rp = res ? res + static_cast<size_t>(blockIdx.x) * HW : nullptr;
-  for (int i = threadIdx.x; i < HW; i += 256) {
-    float v = act_f((xp[i] - mean) * rstd, act1);
-    if (rp) v = act_f(v + rp[i], act2);
-    op[i] = v;
+  const int tid = threadIdx.x;
+  if constexpr (REG) {
+    float v[IN_MAXN];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < IN_MAXN; ++k) v[k] = tid + 256 * k < HW ? xp[tid + 256 * k] : 0.f;
+#pragma unroll
+    for (int k = 0; k < IN_MAXN; ++k) s += v[k];
+    const float mean = block_sum256(s, red) / static_cast<float>(HW);
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < IN_MAXN; ++k) {
+      const float d = tid + 256 * k < HW ? v[k] - mean : 0.f;
+      s2 = fmaf(d, d, s2);
+    }
+    const float rstd = 1.f / sqrtf(block_sum256(s2, red) / static_cast<float>(HW) + eps);
+#pragma unroll
+    for (int k = 0; k < IN_MAXN; ++k) {
+      const int i = tid + 256 * k;
+      if (i < HW) {
+        float y = act_f((v[k] - mean) * rstd, act1);
+        if (rp) y = act_f(y + rp[i], act2);
+        op[i] = y;
+      }
+    }
+  } else {
+    float s = 0.f;
+    for (int i = tid; i < HW; i += 256) s += xp[i];
+    const float mean = block_sum256(s, red) / static_cast<float>(HW);
+    float s2 = 0.f;
+    for (int i = tid; i < HW; i += 256) {
+      const float d = xp[i] - mean;
+      s2 = fmaf(d, d, s2);
+    }
+    const float rstd = 1.f / sqrtf(block_sum256(s2, red) / static_cast<float>(HW) + eps);
+    for (int i = tid; i < HW; i += 256) {
+      float y = act_f((xp[i] - mean) * rstd, act1);
+      if (rp) y = act_f(y + rp[i], act2);
+      op[i] = y;
+    }
   }
 }
 
@@ -402,26 +510,32 @@ __global__ __launch_bounds__(256) void ew_kernel(const float* __restrict__ a, co
 //   attn = softmax_j( <q_i, k_j> / (max(|q_i|, 1e-12) max(|k_j|, 1e-12)) * temperature[h] ),
 //   out_i = sum_j attn_ij v_j,
 // on the channel-major qkv (B, 3C, N) of its qkv 1x1 conv (q / k / v channel h*ch + i of their third).
-// xca_attn_kernel: one block per (image, head) accumulates the Gram matrix and the row norms over
-// 256-token chunks staged in LDS, then writes the softmaxed ch x ch map; xca_apply_kernel: one thread
-// per token applies it to the v column.  ch <= 40.
-constexpr int XCA_MAXCH = 40, XCA_NC = 128;
+// xca_gram_kernel: block (image, head, split) accumulates the Gram matrix <q_i, k_j> and the squared
+// row norms over its 1/XCA_NS of the tokens (128-token chunks staged in LDS, one thread per pair) into
+// a partial; xca_softmax_kernel: one block per (image, head) sums the XCA_NS partials in split order and
+// writes the softmaxed ch x ch map; xca_apply_kernel: one thread per token applies it to the v column.
+// ch <= 40.  (Round 6: one block per (image, head) -- 16 blocks for the whole chip -- took 153 us at the
+// 1/8-resolution stage; the split spreads the same pairs over B * heads * 16 blocks.)
+constexpr int XCA_MAXCH = 40, XCA_NC = 128, XCA_NS = 16;
+constexpr int XCA_NPAIR = XCA_MAXCH * XCA_MAXCH + 2 * XCA_MAXCH;
 
-__global__ __launch_bounds__(256) void xca_attn_kernel(const float* __restrict__ qkv, const float* __restrict__ temp,
-                                                       float* __restrict__ attn, int C, int nh, int N) {
+__global__ __launch_bounds__(256) void xca_gram_kernel(const float* __restrict__ qkv, float* __restrict__ part, int C,
+                                                       int nh, int N) {
   __shared__ float qs[XCA_MAXCH][XCA_NC + 1];
   __shared__ float ks[XCA_MAXCH][XCA_NC + 1];
-  __shared__ float g[XCA_MAXCH * XCA_MAXCH + 2 * XCA_MAXCH];
-  const int ch = C / nh, h = blockIdx.x % nh, b = blockIdx.x / nh;
+  const int ch = C / nh;
+  const int bh = blockIdx.x / XCA_NS, sp = blockIdx.x - bh * XCA_NS, h = bh % nh, b = bh / nh;
   const int npair = ch * ch + 2 * ch;
+  const int per = (N + XCA_NS - 1) / XCA_NS;
+  const int t_begin = sp * per, t_end = min(N, t_begin + per);
   const float* q = qkv + (static_cast<size_t>(b) * 3 * C + static_cast<size_t>(h) * ch) * N;
   const float* k = q + static_cast<size_t>(C) * N;
-  float acc[(XCA_MAXCH * XCA_MAXCH + 2 * XCA_MAXCH + 255) / 256];
-  constexpr int NP = (XCA_MAXCH * XCA_MAXCH + 2 * XCA_MAXCH + 255) / 256;
+  constexpr int NP = (XCA_NPAIR + 255) / 256;
+  float acc[NP];
 #pragma unroll
   for (int u = 0; u < NP; ++u) acc[u] = 0.f;
-  for (int n0 = 0; n0 < N; n0 += XCA_NC) {
-    const int nc = min(XCA_NC, N - n0);
+  for (int n0 = t_begin; n0 < t_end; n0 += XCA_NC) {
+    const int nc = min(XCA_NC, t_end - n0);
     __syncthreads();
     for (int e = threadIdx.x; e < ch * XCA_NC; e += 256) {
       const int i = e / XCA_NC, t = e - i * XCA_NC;
@@ -433,30 +547,46 @@ __global__ __launch_bounds__(256) void xca_attn_kernel(const float* __restrict__
     for (int u = 0; u < NP; ++u) {
       const int pr = u * 256 + threadIdx.x;
       if (pr >= npair) break;
-      const float* a;
-      const float* c;
+      const float* x;
+      const float* y;
       if (pr < ch * ch) {
-        a = qs[pr / ch];
-        c = ks[pr % ch];
+        x = qs[pr / ch];
+        y = ks[pr % ch];
       } else if (pr < ch * ch + ch) {
-        a = c = qs[pr - ch * ch];
+        x = y = qs[pr - ch * ch];
       } else {
-        a = c = ks[pr - ch * ch - ch];
+        x = y = ks[pr - ch * ch - ch];
       }
       float s = acc[u];
-      for (int t = 0; t < nc; ++t) s = fmaf(a[t], c[t], s);
+      for (int t = 0; t < nc; ++t) s = fmaf(x[t], y[t], s);
       acc[u] = s;
     }
   }
+  float* pp = part + static_cast<size_t>(blockIdx.x) * npair;
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
     const int pr = u * 256 + threadIdx.x;
-    if (pr < npair) g[pr] = acc[u];
+    if (pr < npair) pp[pr] = acc[u];
+  }
+}
+
+__global__ __launch_bounds__(256) void xca_softmax_kernel(const float* __restrict__ part,
+                                                          const float* __restrict__ temp, float* __restrict__ attn,
+                                                          int C, int nh) {
+  __shared__ float g[XCA_NPAIR];
+  const int ch = C / nh, bh = blockIdx.x, h = bh % nh;
+  const int npair = ch * ch + 2 * ch;
+  const float* pp = part + static_cast<size_t>(bh) * XCA_NS * npair;
+  for (int pr = threadIdx.x; pr < npair; pr += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int sp = 0; sp < XCA_NS; ++sp) s += pp[sp * npair + pr];
+    g[pr] = s;
   }
   __syncthreads();
   // row i: softmax over j of the normalised scores (one thread per row)
   const float tp = temp[h];
-  float* ap = attn + (static_cast<size_t>(b) * nh + h) * ch * ch;
+  float* ap = attn + static_cast<size_t>(bh) * ch * ch;
   if (threadIdx.x < ch) {
     const int i = threadIdx.x;
     const float qn = fmaxf(sqrtf(g[ch * ch + i]), 1e-12f);
@@ -512,6 +642,7 @@ extern "C" int fsmi_channel_layernorm(const float* x, float* out, const float* w
   FSMI_CHECK_ARG(B > 0 && C > 0 && n > 0 && n <= Tx && n <= To, "fsmi_channel_layernorm: bad shape (n %d, Tx %d, To %d)",
                  n, Tx, To);
   FSMI_CHECK_ARG(x != out || Tx == To, "fsmi_channel_layernorm: in place needs Tx == To");
+  FSMI_CHECK_ARG(C <= LN_G * LN_MAXN, "fsmi_channel_layernorm: C %d > %d", C, LN_G * LN_MAXN);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_NORM, s);
   const int ntiles = (n + LN_TB - 1) / LN_TB;
@@ -520,26 +651,37 @@ extern "C" int fsmi_channel_layernorm(const float* x, float* out, const float* w
   return finish_launch("fsmi_channel_layernorm");
 }
 
+extern "C" long long fsmi_vit_attention_ws_floats(int B, int heads, int T, int Tp) {
+  if (B <= 0 || heads <= 0 || T <= 0 || Tp <= 0) return 0;
+  int kbs = 0;
+  const int ns = vit_attn_splits(B, heads, T, Tp, &kbs);
+  return ns > 1 ? static_cast<long long>(ns) * B * heads * (ATT_HD + 2) * Tp : 0;
+}
+
 extern "C" int fsmi_vit_attention(const float* qkv, float* out, int B, int heads, int head_dim, int T, int Tp,
-                                  float scale, void* stream) {
+                                  float scale, float* ws, long long ws_floats, void* stream) {
   FSMI_CHECK_ARG(qkv && out && qkv != out, "fsmi_vit_attention: null or aliased pointers");
   FSMI_CHECK_ARG(head_dim == ATT_HD, "fsmi_vit_attention: head dim %d (built for 64)", head_dim);
   FSMI_CHECK_ARG(B > 0 && heads > 0 && T > 0 && T <= Tp && Tp % ATT_KB == 0,
                  "fsmi_vit_attention: T %d, Tp %d (Tp a multiple of %d, T <= Tp)", T, Tp, ATT_KB);
   FSMI_CHECK_ARG(reinterpret_cast<uintptr_t>(qkv) % 16 == 0, "fsmi_vit_attention: qkv must be 16-B aligned");
+  const long long need = fsmi_vit_attention_ws_floats(B, heads, T, Tp);
+  FSMI_CHECK_ARG(ws_floats >= need && (need == 0 || ws), "fsmi_vit_attention: workspace %lld floats < %lld",
+                 ws_floats, need);
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_DT, s);
   const float qs = scale * 1.4426950408889634f;
-  // 4 waves (128 queries) per block when that still gives >= 2 blocks per CU, else 2 waves
-  const long long nb4 = static_cast<long long>(B) * heads * ((Tp + 127) / 128);
-  if (nb4 >= 512) {
-    const int nqt = (Tp + 127) / 128;
-    hipLaunchKernelGGL(vit_attn_kernel<4>, dim3(static_cast<unsigned>(B * heads * nqt)), dim3(256), 0, s, qkv, out,
-                       heads, T, Tp, qs, nqt);
-  } else {
-    const int nqt = (Tp + 63) / 64;
-    hipLaunchKernelGGL(vit_attn_kernel<2>, dim3(static_cast<unsigned>(B * heads * nqt)), dim3(128), 0, s, qkv, out,
-                       heads, T, Tp, qs, nqt);
+  int kbs = 0;
+  const int ns = vit_attn_splits(B, heads, T, Tp, &kbs);
+  const int nqt = (Tp + 127) / 128;
+  float* opart = ns > 1 ? ws : nullptr;
+  float* mlpart = ns > 1 ? ws + static_cast<size_t>(ns) * B * heads * ATT_HD * Tp : nullptr;
+  hipLaunchKernelGGL(vit_attn_kernel<4>, dim3(static_cast<unsigned>(B * heads * nqt * ns)), dim3(256), 0, s, qkv, out,
+                     heads, T, Tp, qs, nqt, ns, kbs, opart, mlpart);
+  if (ns > 1) {
+    const long long n = static_cast<long long>(B) * heads * (ATT_HD / 8) * Tp;
+    hipLaunchKernelGGL(vit_attn_combine_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, opart,
+                       mlpart, out, B * heads, Tp, ns);
   }
   return finish_launch("fsmi_vit_attention");
 }
@@ -594,8 +736,12 @@ extern "C" int fsmi_instance_norm(const float* x, const float* res, float* out, 
                  "fsmi_instance_norm: act 0 / 1 / 6");
   hipStream_t s = as_stream(stream);
   LaunchTimer t(FSMI_K_NORM, s);
-  hipLaunchKernelGGL(instnorm_kernel, dim3(static_cast<unsigned>(planes)), dim3(256), 0, s, x, res, out, HW, eps, act1,
-                     act2);
+  if (HW <= 256 * IN_MAXN)
+    hipLaunchKernelGGL(instnorm_kernel<true>, dim3(static_cast<unsigned>(planes)), dim3(256), 0, s, x, res, out, HW,
+                       eps, act1, act2);
+  else
+    hipLaunchKernelGGL(instnorm_kernel<false>, dim3(static_cast<unsigned>(planes)), dim3(256), 0, s, x, res, out, HW,
+                       eps, act1, act2);
   return finish_launch("fsmi_instance_norm");
 }
 
@@ -608,16 +754,27 @@ extern "C" int fsmi_elementwise(const float* a, const float* b, float* out, long
   return finish_launch("fsmi_elementwise");
 }
 
-extern "C" int fsmi_xca(const float* qkv, const float* temperature, float* attn_ws, float* out, int B, int C, int heads,
+extern "C" long long fsmi_xca_workspace_floats(int B, int C, int heads) {
+  if (B <= 0 || heads <= 0 || C % heads) return 0;
+  const long long ch = C / heads;
+  return static_cast<long long>(B) * heads * (ch * ch + XCA_NS * (ch * ch + 2 * ch));
+}
+
+extern "C" int fsmi_xca(const float* qkv, const float* temperature, float* ws, float* out, int B, int C, int heads,
                         int N, void* stream) {
-  FSMI_CHECK_ARG(qkv && temperature && attn_ws && out && out != qkv, "fsmi_xca: null or aliased pointers");
+  FSMI_CHECK_ARG(qkv && temperature && ws && out && out != qkv, "fsmi_xca: null or aliased pointers");
   FSMI_CHECK_ARG(B > 0 && heads > 0 && N > 0 && C % heads == 0 && C / heads <= XCA_MAXCH,
                  "fsmi_xca: C %d over %d heads (<= %d channels per head)", C, heads, XCA_MAXCH);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(xca_attn_kernel, dim3(static_cast<unsigned>(B * heads)), dim3(256), 0, s, qkv, temperature,
-                     attn_ws, C, heads, N);
+  const int ch = C / heads;
+  float* attn = ws;                                          // B * heads * ch * ch
+  float* part = ws + static_cast<size_t>(B) * heads * ch * ch;   // B * heads * XCA_NS * (ch * ch + 2 ch)
+  hipLaunchKernelGGL(xca_gram_kernel, dim3(static_cast<unsigned>(B * heads * XCA_NS)), dim3(256), 0, s, qkv, part,
+                     C, heads, N);
+  hipLaunchKernelGGL(xca_softmax_kernel, dim3(static_cast<unsigned>(B * heads)), dim3(256), 0, s, part, temperature,
+                     attn, C, heads);
   const int ntile = (N + 255) / 256;
-  hipLaunchKernelGGL(xca_apply_kernel, dim3(static_cast<unsigned>(B * heads * ntile)), dim3(256), 0, s, qkv, attn_ws,
+  hipLaunchKernelGGL(xca_apply_kernel, dim3(static_cast<unsigned>(B * heads * ntile)), dim3(256), 0, s, qkv, attn,
                      out, C, heads, N, ntile);
   return finish_launch("fsmi_xca");
 }

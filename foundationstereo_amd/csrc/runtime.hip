@@ -401,6 +401,13 @@ int fsmi_timer_dump_captured(char* buf, long long size, long long* needed) {
   return FSMI_OK;
 }
 
+int fsmi_timer_captured_count(long long* n) {
+  FSMI_CHECK_ARG(n, "fsmi_timer_captured_count: null pointer");
+  std::lock_guard<std::mutex> lk(fsmi::g_mu);
+  *n = static_cast<long long>(fsmi::g_clock_caplog.size());
+  return FSMI_OK;
+}
+
 int fsmi_timer_release_captured(void) {
   std::lock_guard<std::mutex> lk(fsmi::g_mu);
   for (auto& v : fsmi::g_clock_captured) v.clear();

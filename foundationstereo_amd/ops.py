@@ -974,6 +974,14 @@ def timer_dump_captured():
     return out
 
 
+def timer_captured_count():
+    """Launches captured with clocks so far; no device work, so callable inside a capture."""
+    import ctypes
+    n = ctypes.c_longlong(0)
+    _lib.check(_lib.load().fsmi_timer_captured_count(ctypes.byref(n)), "timer_captured_count")
+    return n.value
+
+
 def timer_release_captured():
     """Forget the clock records of captured launches and free their slots; only once every graph
     captured with ``in_capture=True`` is destroyed (include/fsmi.h)."""
@@ -1030,8 +1038,11 @@ def vit_attention(qkv: Tensor, heads: int, T: int, scale: float, out: Tensor = N
     if out is None:
         out = torch.empty((B, heads * hd) + tuple(qkv.shape[2:]), device=qkv.device, dtype=torch.float32)
     _check("vit_attention", out)
-    _lib.check(_lib.load().fsmi_vit_attention(_p(qkv), _p(out), B, heads, hd, int(T), Tp, float(scale),
-                                              _stream(qkv)), "vit_attention")
+    lib = _lib.load()
+    nws = int(lib.fsmi_vit_attention_ws_floats(B, heads, int(T), Tp))
+    ws = torch.empty(max(nws, 1), device=qkv.device, dtype=torch.float32)
+    _lib.check(lib.fsmi_vit_attention(_p(qkv), _p(out), B, heads, hd, int(T), Tp, float(scale), _p(ws), nws,
+                                      _stream(qkv)), "vit_attention")
     return out
 
 
@@ -1130,8 +1141,8 @@ def xca(qkv: Tensor, temperature: Tensor, heads: int) -> Tensor:
     C = C3 // 3
     qkv = _c(qkv)
     N = qkv[0, 0].numel()
-    ch = C // heads
-    ws = torch.empty(B * heads * ch * ch, device=qkv.device, dtype=torch.float32)
+    nws = _lib.load().fsmi_xca_workspace_floats(B, C, heads)
+    ws = torch.empty(max(int(nws), 1), device=qkv.device, dtype=torch.float32)
     out = torch.empty((B, C) + tuple(qkv.shape[2:]), device=qkv.device, dtype=torch.float32)
     _lib.check(_lib.load().fsmi_xca(_p(qkv), _p(t), _p(ws), _p(out), B, C, heads, N, _stream(qkv)), "xca")
     return out

@@ -107,7 +107,14 @@ def _side_stream(device, idx=0):
 # progress it records the waits between side streams and raises before a wait that would close a cycle
 # (X waiting on A after A waited on X, directly or through other side streams) -- every variant the
 # probe saw segfault has such a mutual wait, every variant that passed has none.
-_CAPTURE_EDGES = {}          # id(waiter) -> set of id(waited), side streams only, current capture
+_CAPTURE_EDGES = {}          # key(waiter) -> set of key(waited), side streams only, current capture
+
+
+def _skey(s):
+    """A stream's identity: its HIP handle (torch.cuda.current_stream() returns a new Python wrapper on
+    every call, so id() of the wrapper does not identify the stream); id() for handle-less stand-ins."""
+    h = getattr(s, "cuda_stream", None)
+    return ("hip", h) if h is not None else ("obj", id(s))
 
 
 class CaptureForkError(RuntimeError):
@@ -117,13 +124,13 @@ class CaptureForkError(RuntimeError):
 def capture_fork_check(waiter, waited, capturing: bool, side_ids=None):
     """Record ``waiter`` waiting on ``waited`` for the capture in progress; raise CaptureForkError when
     ``waited`` already (transitively) waits on ``waiter``.  Only edges between side streams count (the
-    capture origin forks and joins every side stream).  ``side_ids``: ids of the side streams (default
+    capture origin forks and joins every side stream).  ``side_ids``: ``_skey`` of the side streams (default
     the ones ``_side_stream`` made).  Not capturing: forget the edges (a new capture starts clean)."""
     if not capturing:
         _CAPTURE_EDGES.clear()
         return
-    side = side_ids if side_ids is not None else {id(v) for v in _SIDE.values()}
-    a, b = id(waiter), id(waited)
+    side = side_ids if side_ids is not None else {_skey(v) for v in _SIDE.values()}
+    a, b = _skey(waiter), _skey(waited)
     if a == b or a not in side or b not in side:
         return
     seen, todo = set(), [b]
@@ -150,7 +157,7 @@ def stream_wait(waiter, waited):
     capturing = torch.cuda.is_current_stream_capturing()
     capture_fork_check(waiter, waited, capturing)
     if WAIT_LOG is not None and capturing:
-        WAIT_LOG.append((waiter.cuda_stream, waited.cuda_stream, len(ops.timer_dump_captured())))
+        WAIT_LOG.append((waiter.cuda_stream, waited.cuda_stream, ops.timer_captured_count()))
     waiter.wait_stream(waited)
 
 

@@ -321,7 +321,8 @@ int fsmi_upsample4_add(const float* t, float* vol, int B, int C, int D, int H, i
  *   (Tx = To = n = H*W).
  * fsmi_vit_attention: softmax(q k^T * scale) v per head (layers/attention.py:69-79): qkv (B, 3*heads*64, Tp)
  *   = [q; k; v] channel-major, out (B, heads*64, Tp); keys >= T masked; head_dim 64; Tp % 64 == 0.
- *   Split-precision MFMA (3 fp16 products per MAC), fp32 softmax.
+ *   Split-precision MFMA (3 fp16 products per MAC), fp32 softmax.  ws: fsmi_vit_attention_ws_floats(B, heads,
+ *   T, Tp) floats (0: NULL allowed) for the key-range partials when the keys are split over several blocks.
  * fsmi_space_to_depth: out[b, (c*k+ky)*k+kx, y, x] = x[b, c, y*k+ky, x*k+kx] (B,C,H,W) -> (B,C*k*k,H/k,W/k):
  *   the im2col of a conv with stride == kernel (patch embed k14, EdgeNeXt stem k4 / downsample k2).
  * fsmi_depth_to_space: out[b, c, y*k+ky, x*k+kx] = x[b, (ky*k+kx)*C + c, y, x]: a ConvTranspose2d with
@@ -335,13 +336,15 @@ int fsmi_upsample4_add(const float* t, float* vol, int B, int C, int D, int H, i
  *   core/extractor.py:20-80 with norm 'instance').
  * fsmi_elementwise: op 0 a+b, 1 relu(a), 2 relu(a+b), 3 a*b; b indexed modulo bper when bper > 0.
  * fsmi_xca: EdgeNeXt cross-covariance attention core (timm CrossCovarianceAttn): qkv (B,3C,N) channel-major,
- *   temperature (heads), attn_ws (B*heads*(C/heads)^2 floats), out (B,C,N); C/heads <= 40.
+ *   temperature (heads), ws (fsmi_xca_workspace_floats(B, C, heads) floats: the softmaxed maps, then the
+ *   per-split Gram partials), out (B,C,N); C/heads <= 40.
  * fsmi_dwconv2d_ex: fsmi_dwconv2d on channel slices (x / add / out planes at (b*ctot + c)*H*W), KS in
  *   {3,5,7,9}, with add (or NULL) summed into the input first. */
 int fsmi_channel_layernorm(const float* x, float* out, const float* w, const float* b, int B, int C, int Tx, int To,
                            int n, float eps, void* stream);
 int fsmi_vit_attention(const float* qkv, float* out, int B, int heads, int head_dim, int T, int Tp, float scale,
-                       void* stream);
+                       float* ws, long long ws_floats, void* stream);
+long long fsmi_vit_attention_ws_floats(int B, int heads, int T, int Tp);
 int fsmi_space_to_depth(const float* x, float* out, int B, int C, int H, int W, int k, void* stream);
 int fsmi_depth_to_space(const float* x, float* out, int B, int C, int H, int W, int k, void* stream);
 int fsmi_vit_tokens(const float* emb, const float* cls, const float* pos, float* out, int B, int C, int N, int Tp,
@@ -350,8 +353,9 @@ int fsmi_resize_bicubic(const float* x, float* out, int B, int C, int Hi, int Wi
 int fsmi_instance_norm(const float* x, const float* res, float* out, int planes, int HW, float eps, int act1, int act2,
                        void* stream);
 int fsmi_elementwise(const float* a, const float* b, float* out, long long n, long long bper, int op, void* stream);
-int fsmi_xca(const float* qkv, const float* temperature, float* attn_ws, float* out, int B, int C, int heads, int N,
+int fsmi_xca(const float* qkv, const float* temperature, float* ws, float* out, int B, int C, int heads, int N,
              void* stream);
+long long fsmi_xca_workspace_floats(int B, int C, int heads);
 int fsmi_dwconv2d_ex(const float* x, int x_ctot, const float* add, int add_ctot, const float* w, const float* bias,
                      float* out, int out_ctot, int B, int C, int KS, int H, int W, void* stream);
 
@@ -409,6 +413,10 @@ int fsmi_timer_release_captured(void);
  * full length + 1.  Instrumented: the halo / pointwise conv kernels and their split-K reduce, the
  * EdgeNeXt MLP, depthwise / 1-input convs, pool / resize, and the geometry kernels. */
 int fsmi_timer_dump_captured(char* buf, long long size, long long* needed);
+/* The number of lines fsmi_timer_dump_captured would print so far (launches captured with clocks),
+ * without touching the device: callable while a capture is in progress (positions a cross-stream wait
+ * among the captured launches; tools/replay_timeline.py). */
+int fsmi_timer_captured_count(long long* n);
 /* Re-issue the last timed launch of `kernel` (lookup, cost-volume build) `reps` times back to
  * back on its stream between two hipEvents; *avg_ms = span / reps.  The kernels are pure
  * functions of their inputs, so the replays rewrite identical outputs.

@@ -68,7 +68,10 @@ def _sdpa_ref(qkv, heads, T, scale):
     return torch.einsum("bhij,bhdj->bhdi", p, v[..., :T]).reshape(B, heads * hd, Tp)
 
 
-@pytest.mark.parametrize("B,heads,T,Tp", [(2, 6, 21, 64), (2, 6, 150, 192), (1, 16, 1921, 1984), (4, 16, 700, 704)])
+# key ranges per (image, head, query tile) (fsmi_vit_attention_ws_floats > 0): 1 (64, 192), 2 (1x16 heads
+# 1984, 4x16 704), 3 (2x6 heads 1984: ViT-S at cfg2), 6 (1x6 heads 1984)
+@pytest.mark.parametrize("B,heads,T,Tp", [(2, 6, 21, 64), (2, 6, 150, 192), (1, 16, 1921, 1984), (4, 16, 700, 704),
+                                          (2, 6, 1921, 1984), (1, 6, 1900, 1984)])
 def test_vit_attention(B, heads, T, Tp):
     qkv = _rand((B, 3 * heads * 64, Tp), 4, 1.5)
     out = ops.vit_attention(qkv.to(DEV), heads, T, 0.125)
@@ -111,12 +114,16 @@ def test_deconv_as_depth_to_space(k, C):
 def test_resize_bicubic(Hi, Wi, Ho, Wo):
     x = _rand((2, 3, Hi, Wi), 10, 2.0)
     out = ops.resize_bicubic(x.to(DEV), (Ho, Wo))
-    # the reference runs it in fp32 (source coordinates from the fp32 in/out scale): agree with that to
-    # rounding, and with the fp64 interpolation to the fp32 coordinate error (~1e-5 relative)
+    # the reference runs it in fp32 (source coordinates from the fp32 in/out scale, one fma rounding):
+    # agree with that to rounding; against the fp64 interpolation, be no further than the reference's
+    # own fp32 result is (its fp32 source coordinate is off by up to an ulp of a few hundred pixels,
+    # which on this noise moves outputs by up to ~5e-5 relative)
     ref32 = F.interpolate(x, size=(Ho, Wo), mode="bicubic", align_corners=False)
     _close(out, ref32, rel=5e-6, abs_=1e-6, what="bicubic vs fp32")
     ref = F.interpolate(x.double(), size=(Ho, Wo), mode="bicubic", align_corners=False)
-    _close(out, ref, rel=2e-5, abs_=1e-6, what="bicubic vs fp64")
+    e32, _ = _err(ref32, ref)
+    e, m = _err(out, ref)
+    assert e <= 1.1 * e32 + 2e-6 * m, f"bicubic vs fp64: {e:.3g}, the reference's fp32 path {e32:.3g}"
 
 
 @pytest.mark.parametrize("act,res,act2", [(None, False, None), ("leaky", False, None), ("relu", True, "relu"),

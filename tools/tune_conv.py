@@ -4,6 +4,7 @@ and MERGE them into tuning/fsmi_conv.json (read by ops.conv2d / conv2d_gate / co
 caller leaves cfg / nsplit on auto).  Run on the GPU box:
 
     python tools/tune_conv.py [--config cfg2 cfg3 ...] [--reps 5] [--only-cfgs 19 20 21 23]
+    python tools/tune_conv.py --with-backbone --new-only     # the backbone's (Feature) conv shapes
 
 Candidates per shape: the plain tiles (0-9 as they apply), the K-group variants (16 + 3/4/5/7:
 two wave groups per block on alternate chunks, summed in LDS), for 2D 1x1 layers the pointwise
@@ -35,6 +36,9 @@ ap.add_argument("--only-cfgs", type=int, nargs="*", default=None,
                 help="time only these cfgs (plus the current table entry); keep the better")
 ap.add_argument("--max-split", type=int, default=8, help="largest split-K factor to time")
 ap.add_argument("--match", default="", help="only re-tune shape keys matching this regex (e.g. '_d(?!1_)' volumes)")
+ap.add_argument("--with-backbone", action="store_true",
+                help="record the shapes of a forward WITH the HIP backbone (Feature), not preset features")
+ap.add_argument("--new-only", action="store_true", help="tune only shape keys the table does not hold yet")
 ap.add_argument("--out", default=os.path.join(REPO, "tuning", "fsmi_conv.json"))
 ap.add_argument("--base", default=os.path.join(REPO, "tuning", "fsmi_conv.json"),
                 help="table to start from (merged into --out)")
@@ -48,8 +52,10 @@ def record_shapes(config):
     """Conv shape keys of one (2-iteration) pass of ``config``, tuning table off (all on auto)."""
     H, W, md, iters, vit, per_gpu = bench.CONFIGS[config]
     args = synth.make_args(max_disp=md, corr_levels=4, vit_size=vit)
+    if a.with_backbone:
+        args["backbone"] = "real"
     model = bench.make_model(args, dev, 0)
-    for (ph, pw) in bench.pass_sizes(config, H, W):
+    for (ph, pw) in ([] if a.with_backbone else bench.pass_sizes(config, H, W)):
         feats = [synth.backbone_features(1, ph, pw, vit, seed=0x5EED + i, shift_px=8) for i in range(per_gpu)]
         fl = [torch.from_numpy(np.concatenate([f[0][j] for f in feats])).to(dev) for j in range(4)]
         fr = [torch.from_numpy(np.concatenate([f[1][j] for f in feats])).to(dev) for j in range(4)]
@@ -104,6 +110,8 @@ prev = dict(entries)
 keys = sorted({k for c in a.config for k in record_shapes(c)})
 if a.match:
     keys = [k for k in keys if re.search(a.match, k)]
+if a.new_only:
+    keys = [k for k in keys if k not in entries]
 print(f"[tune] {len(keys)} conv shapes for {a.config}", file=sys.stderr)
 t_start = time.time()
 with torch.no_grad():
