@@ -216,6 +216,8 @@ __device__ __forceinline__ float sigm_h(float x) { return 1.f / (1.f + expf(-x))
 // packed weight units (x 2^wexp[co]; the split-K partials): v * sb[co].x + sb[co].y, then:
 //  act 0/1/2/6: out[b, co0+co] = res + gamma * alpha * act(v + bias)   (none / ReLU / GELU-erf /
 //               LeakyReLU 0.01); with res_pre: gamma * alpha * act(v + bias + res)
+//  act 7:       out[b, co0+co] = ReLU(v + bias + res) -- 2D maps: the rest of a conv whose other input
+//               channels' contribution (+ bias) was computed once into res (a loop-invariant segment)
 //  act 3 (convz|convr):  co <  Hd: z[b,co] = sigmoid(v + bias);
 //                        co >= Hd: rh[b,co-Hd] = sigmoid(v + bias) * h[b,co-Hd]
 //  act 4 (small convq):  out[b,co0+co] = ((1-z)h + z tanh(v + bias)) * att
@@ -261,9 +263,9 @@ __device__ __forceinline__ void store_el(const HaloArgs& a, float v, int co, int
     const long long P = static_cast<long long>(a.H) * a.W;
     g = sigm_h(a.fatt[(static_cast<long long>(b) * a.Cout + co) * P + hw % P]);
   }
-  if (RESPRE && a.res_pre) {       // ResNet tail: act(v + bias + res)
+  if ((RESPRE && a.res_pre) || a.act == 7) {   // ResNet tail / act 7: act(v + bias + res)
     v += res[b * a.res_bstride + static_cast<long long>(co) * HW + hw];
-    *o = g * (a.act == 1 ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v));
+    *o = g * ((a.act == 1 || a.act == 7) ? fmaxf(v, 0.f) : (a.act == 6 ? (v >= 0.f ? v : 0.01f * v) : v));
     return;
   }
   if (a.act == 1) v = fmaxf(v, 0.f);
@@ -353,7 +355,7 @@ __device__ __forceinline__ void store_frag_c(const HaloArgs& a, const f32x16& v,
     }
     return;
   } else {
-    const bool pre = RESPRE && a.res_pre;
+    const bool pre = (RESPRE && a.res_pre) || ACT == 7;
     // FeatureAtt gate (volumes only): sigmoid(fatt[b, co, hw2]), hw2 = h * W + w of the output plane
     const float* __restrict__ fatt = RESPRE ? a.fatt : nullptr;
     const long long P = static_cast<long long>(a.H) * a.W;
@@ -374,8 +376,8 @@ __device__ __forceinline__ void store_frag_c(const HaloArgs& a, const f32x16& v,
       const int co = cb + (r & 3) + 8 * (r >> 2);
       if (!full && co >= a.Cout) continue;
       float x = v[r] * c.q[r].x + c.q[r].y;
-      if (pre) x += rv[r];         // ResNet tail: act(conv + bias + res)
-      if constexpr (ACT == 1) x = fmaxf(x, 0.f);
+      if (pre) x += rv[r];         // ResNet tail / act 7: act(conv + bias + res)
+      if constexpr (ACT == 1 || ACT == 7) x = fmaxf(x, 0.f);
       else if constexpr (ACT == 2) x = gelu_erf_h(x);
       else if constexpr (ACT == 6) x = x >= 0.f ? x : 0.01f * x;
       if (!pre) x = x * a.alpha * c.g[r] + rv[r];
@@ -444,9 +446,9 @@ __device__ __forceinline__ void store4(const HaloArgs& a, const float (&v)[4], i
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float x = v[k] * q.x + q.y;
-    if (a.res_pre) {             // ResNet tail: act(v + bias + res)
+    if (a.res_pre || a.act == 7) {   // ResNet tail / act 7: act(v + bias + res)
       x += rv[k];
-      x = a.act == 1 ? fmaxf(x, 0.f) : (a.act == 6 ? (x >= 0.f ? x : 0.01f * x) : x);
+      x = (a.act == 1 || a.act == 7) ? fmaxf(x, 0.f) : (a.act == 6 ? (x >= 0.f ? x : 0.01f * x) : x);
     } else {
       if (a.act == 1) x = fmaxf(x, 0.f);
       else if (a.act == 2) x = gelu_erf_h(x);
@@ -861,6 +863,7 @@ __device__ __forceinline__ void conv_epilogue(const HaloArgs& a, const f32x16 (&
     case 4: epi_tile<4, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
     case 5: epi_tile<5, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
     case 6: epi_tile<6, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
+    case 7: epi_tile<7, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
     default: epi_tile<0, TM, TN, D3, UP>(a, acc, xinv, t, wm, wn, lane, fown, lsb, lg); break;
   }
 }

@@ -304,7 +304,9 @@ extern "C" int fsmi_conv2d_halo_x3(const float* const* seg_ptr, const int* seg_c
                                    int KS, int H, int W, int act, float alpha, int cfg, int nsplit, float* ws,
                                    long long ws_floats, void* stream) {
   FSMI_CHECK_ARG(out, "fsmi_conv2d_halo_x3: null output");
-  FSMI_CHECK_ARG((act >= 0 && act <= 2) || act == 6, "fsmi_conv2d_halo_x3: act %d (0, 1, 2, 6)", act);
+  FSMI_CHECK_ARG((act >= 0 && act <= 2) || act == 6 || act == 7, "fsmi_conv2d_halo_x3: act %d (0, 1, 2, 6, 7)", act);
+  FSMI_CHECK_ARG(act != 7 || (res && !gamma && alpha == 1.f), "fsmi_conv2d_halo_x3: act 7 (ReLU(conv + bias + res)) "
+                 "needs res, no gamma, alpha 1");
   HaloArgs a{};
   a.act = act;
   a.alpha = alpha;

@@ -315,6 +315,7 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(HaloArgs a) {
     case 4: epi(std::integral_constant<int, 4>()); break;
     case 5: epi(std::integral_constant<int, 5>()); break;
     case 6: epi(std::integral_constant<int, 6>()); break;
+    case 7: epi(std::integral_constant<int, 7>()); break;
     default: epi(std::integral_constant<int, 0>()); break;
   }
 }

@@ -190,6 +190,68 @@ __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x
   out[i] = hy * top + ly * bot;
 }
 
+
+// Conv2d(Cin, 1, 3, padding=1) + bias (+ res): DispHead's last layer (core/update.py:28), the loop's
+// disp + delta.  One output channel leaves 31 of 32 MFMA rows of a halo tile idle (19 us at cfg2 on
+// the 32-cout tile); here it is a VALU dot product per pixel in fp32: a block is a 2 x 64 pixel tile,
+// its four waves each sum a quarter of the channels (9 taps from global memory, L1-resident) and
+// combine through LDS in wave order (deterministic).
+constexpr int C1O_TR = 2, C1O_TC = 64;
+__global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            float bias, const float* __restrict__ res,
+                                                            long long res_bstride, float* __restrict__ out,
+                                                            long long out_bstride, int Cin, int H, int W, int ntr,
+                                                            int ntc, unsigned long long* clk) {
+  FSMI_TIMELINE_CLOCK(clk);
+  __shared__ float part[4][C1O_TR * C1O_TC];
+  const int b = blockIdx.x / (ntr * ntc);
+  const int t = blockIdx.x - b * ntr * ntc;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = (t % ntc) * C1O_TC + lane, r0 = (t / ntc) * C1O_TR;
+  const int cq = (Cin + 3) / 4, cb = wave * cq, ce = min(Cin, cb + cq);
+  const long long HW = static_cast<long long>(H) * W;
+  const float* xb = x + (static_cast<long long>(b) * Cin) * HW;
+  // per tap: offset and validity of the (r0 + rr + dh - 1, c0 + dw - 1) input pixel, rr in [0, TR)
+  float acc[C1O_TR];
+#pragma unroll
+  for (int rr = 0; rr < C1O_TR; ++rr) acc[rr] = 0.f;
+#pragma unroll 4
+  for (int c = cb; c < ce; ++c) {
+    const float* xc = xb + c * HW;
+    const float* wc = w + c * 9;                   // uniform: scalar loads
+    float v[C1O_TR + 2][3];
+#pragma unroll
+    for (int ir = 0; ir < C1O_TR + 2; ++ir) {
+      const int hh = r0 + ir - 1;
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw) {
+        const int ww = c0 + dw - 1;
+        v[ir][dw] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? xc[hh * W + ww] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < C1O_TR; ++rr)
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) acc[rr] = fmaf(wc[dh * 3 + dw], v[rr + dh][dw], acc[rr]);
+  }
+#pragma unroll
+  for (int rr = 0; rr < C1O_TR; ++rr) part[wave][rr * C1O_TC + lane] = acc[rr];
+  __syncthreads();
+  if (wave < C1O_TR) {
+    const int rr = wave, hh = r0 + rr;
+    if (hh < H && c0 < W) {
+      float s = part[0][rr * C1O_TC + lane];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) s += part[q][rr * C1O_TC + lane];
+      s += bias;
+      const long long p = static_cast<long long>(hh) * W + c0;
+      if (res) s += res[b * res_bstride + p];
+      out[b * out_bstride + p] = s;
+    }
+  }
+}
 }  // namespace
 }  // namespace fsmi
 
@@ -264,4 +326,18 @@ extern "C" int fsmi_resize_bilinear(const float* x, float* out, int B, int C, in
   hipLaunchKernelGGL(resize_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, x, out, planes,
                      Hi, Wi, Ho, Wo, sh, sw, clock_slot(FSMI_K_RESIZE, s, 4ll * ((n + 255) / 256), "resize", true));
   return finish_launch("fsmi_resize_bilinear");
+}
+
+extern "C" int fsmi_conv3x3_cout1(const float* x, int Cin, const float* w, float bias, const float* res,
+                                  long long res_bstride, float* out, long long out_bstride, int B, int H, int W,
+                                  void* stream) {
+  FSMI_CHECK_ARG(x && w && out, "fsmi_conv3x3_cout1: null pointer");
+  FSMI_CHECK_ARG(B > 0 && Cin > 0 && H > 0 && W > 0, "fsmi_conv3x3_cout1: bad shape");
+  hipStream_t s = as_stream(stream);
+  LaunchTimer t(FSMI_K_CONV2D, s);
+  const int ntr = (H + C1O_TR - 1) / C1O_TR, ntc = (W + C1O_TC - 1) / C1O_TC;
+  const unsigned nb = static_cast<unsigned>(B) * ntr * ntc;
+  hipLaunchKernelGGL(conv3x3_cout1_kernel, dim3(nb), dim3(256), 0, s, x, w, bias, res, res_bstride, out, out_bstride,
+                     Cin, H, W, ntr, ntc, clock_slot(FSMI_K_CONV2D, s, 4ll * nb, "conv3x3_cout1", true));
+  return finish_launch("fsmi_conv3x3_cout1");
 }

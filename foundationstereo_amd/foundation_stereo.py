@@ -365,8 +365,10 @@ class FoundationStereo(nn.Module):
                 stream_wait(ctx_s, main)
                 with torch.cuda.stream(ctx_s):
                     stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
+                    ctx_pre = self.update_block.context_pre(inp_list)
             else:
                 stem_2x, net_list, inp_list, att = self._context(image1, vit_feat)
+                ctx_pre = self.update_block.context_pre(inp_list)
             fuse = _sub.FATT_FUSE and not self.training
             gates = None
             if fuse and ctx_s is not None:
@@ -411,7 +413,7 @@ class FoundationStereo(nn.Module):
                 init_disp = ops.softmax_regression(logits)
             if ctx_s is not None:
                 stream_wait(main, ctx_s)
-                for t in [stem_2x, *net_list, *inp_list, *att]:
+                for t in [stem_2x, *net_list, *inp_list, *att, *(ctx_pre or ())]:
                     t.record_stream(main)
 
         if geo_fn is None:
@@ -426,13 +428,13 @@ class FoundationStereo(nn.Module):
         if overlap and test_mode and self.args.n_gru_layers == 3 and iters > 0 and _update.PIPELINE:
             # gru16 / gru08 one iteration ahead on their own stream (same math, see run_pipelined)
             net_list, mask_feat_4, disp = self.update_block.run_pipelined(net_list, inp_list, geo_fn,
-                                                                          disp.detach(), att, iters)
+                                                                          disp.detach(), att, iters, pre=ctx_pre)
             return self.upsample_disp(disp, mask_feat_4, stem_2x)
         for itr in range(iters):
             disp = disp.detach()
             if overlap:    # lookup + motion encoder on a side stream beside gru16/gru08 (same math)
                 net_list, mask_feat_4, delta_disp = self.update_block.forward_overlapped(
-                    net_list, inp_list, geo_fn, disp, att)
+                    net_list, inp_list, geo_fn, disp, att, pre=ctx_pre)
             else:
                 geo_feat = geo_fn(disp)
                 with autocast(mp, md):

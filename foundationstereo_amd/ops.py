@@ -281,7 +281,9 @@ def conv3d_direct(x: Tensor, w: Tensor, bias: Tensor = None) -> Tensor:
     return out
 
 
-ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "leaky": 6}   # leaky: halo kernel only
+# leaky: halo kernel only; relu_pre: ReLU(conv + bias + res), res added BEFORE the activation (2D halo /
+# pointwise tiles; SelectiveConvGRU.conv0 with its loop-invariant context segment precomputed into res)
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "leaky": 6, "relu_pre": 7}
 
 
 class PackedConv:
@@ -729,6 +731,31 @@ def conv2d_1in(x: Tensor, w: Tensor, bias: Tensor = None, relu: bool = False) ->
     out = torch.empty((B, Cout, H, W), device=x.device, dtype=torch.float32)
     _lib.check(_lib.load().fsmi_conv2d_1in(_p(x), _p(w), _p(_c(bias)) if bias is not None else None, _p(out), B,
                                            Cout, KS, H, W, 1 if relu else 0, _stream(x)), "conv2d_1in")
+    return out
+
+
+def conv3x3_cout1(x: Tensor, w: Tensor, bias: Tensor = None, res: Tensor = None, out: Tensor = None,
+                  co0: int = 0) -> Tensor:
+    """``Conv2d(Cin, 1, 3, padding=1)`` (+ bias, + ``res`` (B, 1, H, W)) in fp32 (``fsmi_conv3x3_cout1``):
+    DispHead's last layer.  Writes channel ``co0`` of ``out`` (allocated as (B, 1, H, W) when None)."""
+    _check("conv3x3_cout1", x, w, *[t for t in (bias, res) if t is not None])
+    B, C, H, W = x.shape
+    assert tuple(w.shape) == (1, C, 3, 3), f"conv3x3_cout1: weight {tuple(w.shape)} for {C} channels"
+    x, w = _c(x), _c(w.detach().float())
+    if out is None:
+        out = torch.empty((B, 1, H, W), device=x.device, dtype=torch.float32)
+    assert out.is_contiguous() and out.shape[0] == B and out.shape[2:] == (H, W) and 0 <= co0 < out.shape[1], \
+        "conv3x3_cout1: out must be a contiguous (B, C, H, W) tensor with channel co0"
+    if res is not None:
+        assert res.shape[0] == B and res.shape[1] == 1 and res.shape[2:] == (H, W) and res.stride(2) == W and \
+            res.stride(3) == 1, "conv3x3_cout1: res must be (B, 1, H, W) with dense planes"
+    b = float(bias.detach().float().reshape(-1)[0]) if bias is not None else 0.0
+    HW = H * W
+    _lib.check(_lib.load().fsmi_conv3x3_cout1(
+        _p(x), C, _p(w), b, _p(res) if res is not None else None, res.stride(0) if res is not None else 0,
+        out.data_ptr() + 4 * co0 * HW, out.stride(0), B, H, W, _stream(x)), "conv3x3_cout1")
+    if _CONV_FLOPS["on"]:
+        _CONV_FLOPS["flops"] += 2 * C * 9 * B * HW
     return out
 
 

@@ -41,6 +41,13 @@ PIPE_BRANCH = os.environ.get("FSMI_PIPE_BRANCH", "1") != "0"
 MOTION_ON_MAIN = os.environ.get("FSMI_MOTION_ON_MAIN", "0") != "0"
 
 
+# SelectiveConvGRU.conv0's context segment convolved once per forward (context_pre); 0: every iteration
+CTX_PRE = os.environ.get("FSMI_CTX_PRE", "1") != "0"
+# run_pipelined: gru04's conv0 / conv1 parts that do not depend on the motion path summed in from partial
+# sums computed off the chain (needs CTX_PRE); 0: the whole convs on the chain
+LOOP_PRE = os.environ.get("FSMI_LOOP_PRE", "1") != "0"
+# DispHead's last conv (128 -> 1) on its own fp32 kernel (ops.conv3x3_cout1); 0: the halo conv tile
+COUT1 = os.environ.get("FSMI_COUT1", "1") != "0"
 # the disparity head writes disp + delta into the next encoder buffer (A/B knob)
 HEAD_INPLACE = os.environ.get("FSMI_HEAD_INPLACE", "1") != "0"
 _CONVD1_MIOPEN = os.environ.get("FSMI_CONVD1_MIOPEN", "0") == "1"
@@ -61,11 +68,15 @@ def _f32s(xs):
 def _packed(*mods, cin_order=None):
     """Halo-kernel weights of one Conv2d/Linear (or several stacked along Cout),
     cached on the first module and rebuilt when any weight/bias changes.  ``cin_order``: input
-    channels packed in this order (the caller passes its segments in the same order)."""
+    channels packed in this order (the caller passes its segments in the same order); a subset of
+    the input channels packs the conv restricted to them (one cache entry per order)."""
     key = tuple((id(m), m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version)
                 for m in mods) + (tuple(cin_order) if cin_order is not None else None,)
-    slot = "_fsmi_pack" if cin_order is None else "_fsmi_pack_perm"
-    hit = mods[0].__dict__.get(slot)
+    if cin_order is None:
+        slot, d = "_fsmi_pack", mods[0].__dict__
+    else:
+        slot, d = tuple(cin_order), mods[0].__dict__.setdefault("_fsmi_pack_perm", {})
+    hit = d.get(slot)
     if hit is None or hit[0] != key:
         with torch.no_grad():
             ws = [m.weight if m.weight.dim() == 4 else m.weight[:, :, None, None] for m in mods]
@@ -75,7 +86,7 @@ def _packed(*mods, cin_order=None):
             pk = ops.PackedConv(*ws, mode="halo")
             bias = torch.cat([m.bias.detach().float() for m in mods]).contiguous()
         hit = (key, pk, bias)
-        mods[0].__dict__[slot] = hit
+        d[slot] = hit
     return hit[1], hit[2]
 
 
@@ -217,7 +228,11 @@ class DispHead(nn.Module):
             res = res.float()
             if not res.is_contiguous():
                 res = res.contiguous()
-        return _conv(self.conv[4], [y], res=res, out=out, co0=co0)
+        last = self.conv[4]
+        if COUT1 and last.out_channels == 1 and last.kernel_size == (3, 3):
+            # one output channel: a per-pixel fp32 dot product, not a 32-row MFMA tile
+            return ops.conv3x3_cout1(y, last.weight, last.bias, res=res, out=out, co0=co0)
+        return _conv(last, [y], res=res, out=out, co0=co0)
 
 
 class ConvGRU(nn.Module):
@@ -359,11 +374,74 @@ class SelectiveConvGRU(nn.Module):
         self.small_gru = RaftConvGRU(hidden_dim, input_dim, small_kernel_size)
         self.large_gru = RaftConvGRU(hidden_dim, input_dim, large_kernel_size)
 
-    def forward(self, att, h, *x):
+    def context_pre(self, inp):
+        """conv0's contribution of the context segment plus its bias, ``W0[:, :Ci] * inp + b0``.
+
+        ``x[0]`` of every call is the level's context feature ``inp[i]``, fixed for the whole
+        refinement loop (core/foundation_stereo.py:222-226 build it once; core/update.py:142-151 pass
+        it each iteration), and conv0 is linear in its input channels: this part is computed once
+        per forward and passed back as ``forward(..., pre=)``, which convolves only the remaining
+        channels and adds it before the ReLU (act 7) -- 1/3 (gru04 / gru08) and 1/2 (gru16) of
+        conv0's MACs per iteration.  HIP path only."""
+        inp = _f32(inp)
+        pk, b = _packed(self.conv0[0], cin_order=tuple(range(inp.shape[1])))
+        return ops.conv2d([inp], pk, bias=b)
+
+    def conv0_partial(self, t, c0, res):
+        """``res + W0[:, c0:c0 + C] * t``: one more loop input's part of conv0 (no bias, no activation)
+        added to a partial sum -- run_pipelined folds gru04's upsampled gru08 state into the context
+        part this way on the pipeline stream, as soon as gru08 has produced it."""
+        pk, _ = _packed(self.conv0[0], cin_order=tuple(range(c0, c0 + t.shape[1])))
+        return ops.conv2d([_f32(t)], pk, res=res)
+
+    def conv1_pre(self, h):
+        """``W1[:, Cx:] * h + b1``: conv1's part of the hidden state h (core/update.py:114-115,
+        ``conv1(cat([conv0(x), h]))``), which needs only h -- run_pipelined computes it beside the
+        disparity head and the motion path, off the chain that ends in conv0."""
+        n = self.conv1[0].in_channels
+        pk, b = _packed(self.conv1[0], cin_order=tuple(range(n - h.shape[1], n)))
+        return ops.conv2d([_f32(h)], pk, bias=b)
+
+    def _conv0_rest(self, segs, pre):
+        """ReLU(W0[:, segs] * cat(segs) + pre), ``segs`` the (tensor, conv0 input channel offset) pairs
+        ``pre`` does not cover (see ``context_pre``).  The first segment's LAST 32 channels go first:
+        the motion features (gru04) carry the disparity (~1e2 px) as their last channel, and the kernel
+        fixes a tile's block exponent from its first 32-channel chunk (range mode 2, conv_halo.h
+        chunk_exp), as the motion encoder orders its own cat."""
+        t0, c0 = segs[0]
+        c1 = t0.shape[1]
+        if c1 > 32 and (c1 - 32) % 8 == 0:
+            ss = [(t0, c1 - 32, 32), (t0, 0, c1 - 32)]
+            order = list(range(c0 + c1 - 32, c0 + c1)) + list(range(c0, c0 + c1 - 32))
+        else:
+            ss, order = [t0], list(range(c0, c0 + c1))
+        for t, c in segs[1:]:
+            ss.append(t)
+            order += list(range(c, c + t.shape[1]))
+        pk, _ = _packed(self.conv0[0], cin_order=tuple(order))
+        return ops.conv2d(ss, pk, act="relu_pre", res=pre)
+
+    def forward(self, att, h, *x, pre=None, skip=(0,), pre1=None):
+        """HIP path options (the torch path ignores them; conv0 / conv1 take the whole cats there):
+        ``pre``: conv0's partial sum + bias over the segments ``skip`` of x (``context_pre``, plus
+        ``conv0_partial`` terms); those entries of x are not read and may be given as channel counts.
+        ``pre1``: ``conv1_pre(h)``."""
         if _fast(h):
-            h, x = _f32(h), _f32s(x)
-            xc = _conv(self.conv0[0], list(x), "relu")              # cat(x) as input segments
-            hx = _conv(self.conv1[0], [xc, h], "relu")
+            h = _f32(h)
+            if pre is not None:
+                segs, c = [], 0
+                for i, t in enumerate(x):
+                    if i not in skip:
+                        segs.append((_f32(t), c))
+                    c += t if isinstance(t, int) else t.shape[1]
+                xc = self._conv0_rest(segs, pre)
+            else:
+                xc = _conv(self.conv0[0], _f32s(x), "relu")          # cat(x) as input segments
+            if pre1 is not None:
+                pk, _ = _packed(self.conv1[0], cin_order=tuple(range(self.conv1[0].in_channels - h.shape[1])))
+                hx = ops.conv2d([xc], pk, act="relu_pre", res=pre1)
+            else:
+                hx = _conv(self.conv1[0], [xc, h], "relu")
             # gates in the conv epilogues: z / r*h from the stacked zr convs, then each convq reads
             # [r*h, x] as two segments and blends straight into the new state
             if not FUSED_GATES:
@@ -453,7 +531,16 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         mask = .25 * self.mask(net[0])
         return net, mask, delta_disp
 
-    def forward_overlapped(self, net, inp, geo_fn, disp, att):
+    def context_pre(self, inp):
+        """Per GRU level (gru04, gru08, gru16 as ``inp``), ``SelectiveConvGRU.context_pre`` of its context
+        feature: the loop-invariant part of conv0, computed once per forward (HIP path; None otherwise or
+        with FSMI_CTX_PRE=0)."""
+        if not CTX_PRE or not inp or not _fast(inp[0]):
+            return None
+        grus = [self.gru04, getattr(self, "gru08", None), getattr(self, "gru16", None)]
+        return [g.context_pre(x) for g, x in zip(grus, inp) if g is not None]
+
+    def forward_overlapped(self, net, inp, geo_fn, disp, att, pre=None):
         """``forward(net, inp, geo_fn(disp), disp, att)`` with the motion path -- the lookup and
         the motion encoder, which depend only on ``disp`` -- on a side stream, concurrently with
         gru16 / gru08 (small 1/16 and 1/8 maps that leave most CUs idle).  Joined before gru04.
@@ -468,16 +555,17 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         with torch.cuda.stream(side):
             self.encoder.motion_into(disp, geo_fn, enc)
         n = self.args.n_gru_layers
+        p0, p1, p2 = (list(pre) + [None] * 3)[:3] if pre is not None else (None, None, None)
         if n == 3:
-            net[2] = self.gru16(att[2], net[2], inp[2], pool2x(net[1]))
+            net[2] = self.gru16(att[2], net[2], inp[2], pool2x(net[1]), pre=p2)
         if n >= 2:
             if n > 2:
-                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]), interp(net[2], net[1]))
+                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]), interp(net[2], net[1]), pre=p1)
             else:
-                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]))
+                net[1] = self.gru08(att[1], net[1], inp[1], pool2x(net[0]), pre=p1)
         stream_wait(main, side)
         if n > 1:
-            net[0] = self.gru04(att[0], net[0], inp[0], enc, interp(net[1], net[0]))
+            net[0] = self.gru04(att[0], net[0], inp[0], enc, interp(net[1], net[0]), pre=p0)
         # mask head beside the disparity head (both read net[0] only)
         side1 = _side_stream(disp.device, 1)
         stream_wait(side1, main)
@@ -487,7 +575,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         stream_wait(main, side1)
         return net, mask, delta_disp
 
-    def run_pipelined(self, net, inp, geo_fn, disp, att, iters):
+    def run_pipelined(self, net, inp, geo_fn, disp, att, iters, pre=None):
         """``iters`` refinement iterations (``disp += forward(net, inp, geo_fn(disp), disp, att)[2]``
         each) with gru16 / gru08 running one iteration ahead on a stream of their own.
 
@@ -502,23 +590,46 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         mask head shares the motion stream.  A tensor read on another stream is freed only after
         the freeing stream has joined the reader, so the caching allocator never recycles memory
         a pending kernel still reads.  Returns (net, mask, disp); the mask head runs in the last
-        iteration only (test mode discards the others)."""
+        iteration only (test mode discards the others).  ``pre``: ``context_pre(inp)`` (loop-invariant
+        conv0 parts per level) or None.
+
+        With ``pre`` (and LOOP_PRE) gru04's conv0 and conv1 are split by input channels (conv is linear
+        in them, core/update.py:112-115) so that the chain motion(t) -> gru04(t) -> head(t) carries only
+        the parts that depend on motion(t): conv0 over the motion features alone, conv1 over conv0's
+        output alone.  The rest is summed into their epilogues (act 7) from partial sums computed off
+        the chain: q0 = context part + W0[upsampled gru08(t)] on the pipeline stream right after
+        gru08(t) (its resize moves there too), r1 = W1[h] * n0(t-1) + b1 on the branch stream right
+        after gru04(t-1), beside the disparity head and the motion path."""
         dev = disp.device
         main = torch.cuda.current_stream(dev)
         s_mot, s_gru = _side_stream(dev, 0), _side_stream(dev, 3)
         n0, n1, n2 = net
+        p0, p1, p2 = pre if pre is not None else (None, None, None)
         B, _, H, W = disp.shape
         main_branch = PIPE_BRANCH                        # gru04's small branch on stream 1 (4th stream)
+        nc = self.encoder.conv.out_channels
+        loop_pre = LOOP_PRE and p0 is not None
+        if loop_pre:
+            s_br = _side_stream(dev, 1)
+            c_up = inp[0].shape[1] + nc + 1              # gru04.conv0 input: cat(inp0, motion, interp(n1))
+            g4 = self.gru04
+
+            def r1_next(h):                              # conv1's hidden-state part, on the branch stream
+                stream_wait(s_br, main)
+                with torch.cuda.stream(s_br):
+                    return g4.conv1_pre(h)
+            r1 = r1_next(n0)
         stream_wait(s_gru, main)
         _BRANCH[0] = 0                                   # pipeline-stream GRUs: branches in order
         with torch.cuda.stream(s_gru):
-            n2 = self.gru16(att[2], n2, inp[2], pool2x(n1))
-            n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1))
+            n2 = self.gru16(att[2], n2, inp[2], pool2x(n1), pre=p2)
+            n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1), pre=p1)
+            if loop_pre:
+                q0 = g4.conv0_partial(interp(n1, n0), c_up, p0)
         _BRANCH[0] = 1
         mask = None
         # the disparity lives in the last channel of the encoder output it feeds: the disparity head
         # writes disp + delta straight into the next iteration's buffer (no cat copy, no add pass)
-        nc = self.encoder.conv.out_channels
         enc = disp.new_empty(B, nc + 1, H, W)                                   # on main
         if HEAD_INPLACE:
             enc[:, nc:].copy_(disp)
@@ -532,27 +643,36 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 stream_wait(s_mot, main)
                 with torch.cuda.stream(s_mot):
                     self.encoder.motion_into(disp, geo_fn, enc)
-            stream_wait(main, s_gru)                      # gru08(t): enqueued last on s_gru so far
+            stream_wait(main, s_gru)                      # gru08(t) (+ q0): enqueued last on s_gru so far
             if not MOTION_ON_MAIN:
                 stream_wait(main, s_mot)                  # motion(t)
+            if loop_pre:
+                stream_wait(main, s_br)                   # r1(t)
             if t + 1 < iters:
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru16(t+1), beside gru04(t)
-                    n2 = self.gru16(att[2], n2, inp[2], pool2x(n1))
+                    n2 = self.gru16(att[2], n2, inp[2], pool2x(n1), pre=p2)
                     # gru08(t+1)'s upsampled gru16 input, also beside gru04(t): one kernel less between
                     # gru04(t) and gru08(t+1)
                     up2 = interp(n2, n1) if EARLY_INTERP else None
                 _BRANCH[0] = 1
             _BRANCH[0] = 1 if main_branch else 0
-            n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0))
+            if loop_pre:
+                n0 = g4(att[0], n0, inp[0].shape[1], enc, n1.shape[1], pre=q0, skip=(0, 2), pre1=r1)
+            else:
+                n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0), pre=p0)
             _BRANCH[0] = 1
+            if loop_pre and t + 1 < iters:
+                r1 = r1_next(n0)
             if t + 1 < iters:
                 stream_wait(s_gru, main)                  # gru04(t)
                 # gru08's branches in order on the pipeline stream: a fork from it would be a side
                 # stream waiting on the pipeline stream and waited on by it (capture_fork)
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru08(t+1), beside the heads + motion(t+1)
-                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1))
+                    n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1), pre=p1)
+                    if loop_pre:
+                        q0 = g4.conv0_partial(interp(n1, n0), c_up, p0)
                 _BRANCH[0] = 1
             if t + 1 == iters:
                 # test mode upsamples only the last iteration's disparity: the reference computes the

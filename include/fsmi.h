@@ -155,6 +155,9 @@ int fsmi_conv3d_direct(const float* x, const float* w, const float* bias, float*
  * out[b, co0+co] (tensor with out_ctot channels) =
  *   res[b,co] + gamma[co] * alpha * act(conv + bias[co]);  act 0 none, 1 ReLU, 2 GELU(erf),
  *   6 LeakyReLU 0.01; gamma/res may be NULL (res has res_ctot channels per image).
+ *   act 7: out = ReLU(conv + bias[co] + res[b,co]) (res required, gamma NULL, alpha 1): the
+ *   remaining input channels of a conv whose loop-invariant channels were convolved once
+ *   into res (SelectiveConvGRU.conv0's context segment, core/update.py:112-113).
  * Split-precision operands on the fp16 MFMA ("3 x fp16"): x = hi + lo (two fp16),
  * product = hi*hi + hi*lo + lo*hi accumulated in fp32 (~22-bit operands).  whi/wlo:
  * _Float16 weights packed [KS*KS][Cin32/32][Cout32][32] (Cin32/Cout32 = Cin/Cout rounded
@@ -279,6 +282,13 @@ int fsmi_edgenext_mlp(const float* x, const float* res, float* out, const void* 
                       const float* sb1, const void* w2hi, const void* w2lo, const float* sb2, const float* gamma,
                       int B, int C, int E, int H, int W, void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
+/* fsmi_conv3x3_cout1: Conv2d(Cin, 1, 3, padding=1) + bias (+ res) in fp32 on (B,Cin,H,W) (dense NCHW):
+ * out[b*out_bstride + p] = res[b*res_bstride + p] + bias + sum_c,tap w[c*9 + tap] * x[b, c, p + tap];
+ * res may be NULL.  DispHead's last layer (core/update.py:28), whose caller adds disp (the loop's
+ * disp + delta, core/foundation_stereo.py:240-241) and writes it into the next motion-feature buffer. */
+int fsmi_conv3x3_cout1(const float* x, int Cin, const float* w, float bias, const float* res, long long res_bstride,
+                       float* out, long long out_bstride, int B, int H, int W, void* stream);
+
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->
  *   (B,Cout,H,W): the motion encoder's convd1 + ReLU (core/update.py:57,67); KS in {3,5,7}. */
 int fsmi_conv2d_1in(const float* x, const float* w, const float* bias, float* out, int B, int Cout, int KS,

@@ -845,6 +845,21 @@ def test_selective_gru_fused_vs_oracle(ops_mod, HW):
     close(out, ref, atol=2e-5)
 
 
+@pytest.mark.parametrize("B,C,H,W", [(1, 128, 120, 160), (2, 128, 13, 70), (1, 40, 5, 3)])
+def test_conv3x3_cout1_vs_torch(ops_mod, B, C, H, W):
+    """DispHead's last conv (Cin -> 1, 3x3) on its fp32 kernel, + res, written into a channel slice."""
+    x = g(synth.normal(synth.name_seed(f"c1x{B}{C}{H}"), (B, C, H, W)))
+    w = g(synth.normal(synth.name_seed(f"c1w{B}{C}{H}"), (1, C, 3, 3), 0.05))
+    bias = g(synth.normal(7, (1,), 0.3))
+    res = g(synth.normal(synth.name_seed(f"c1r{B}{C}{H}"), (B, 1, H, W), 20.0))
+    out = torch.full((B, 5, H, W), 7.0, device=DEV)
+    ops_mod.conv3x3_cout1(x, w, bias, res=res, out=out, co0=3)
+    ref = F.conv2d(x.double(), w.double(), bias.double(), padding=1) + res.double()
+    close(out[:, 3:4], ref, atol=2e-5 + 1e-6 * float(ref.abs().max()))
+    assert bool((out[:, :3] == 7.0).all()) and bool((out[:, 4:] == 7.0).all())
+    close(ops_mod.conv3x3_cout1(x, w), F.conv2d(x.double(), w.double(), padding=1), atol=2e-5)
+
+
 def test_update_step_golden(ops_mod):
     gd = load_golden("update_step")
     from foundationstereo_amd.update import BasicSelectiveMultiUpdateBlock
