@@ -64,7 +64,7 @@ SIGNATURES = {
     "fsmi_resize_bilinear": [_P, _P, _I, _I, _I, _I, _I, _I, _P],
     "fsmi_pool2x": [_P, _P, _I, _I, _I, _I, _P],
     "fsmi_conv2d_1in": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
-    "fsmi_conv3x3_cout1": [_P, _I, _P, _F, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _I, _I, _I, _P],
+    "fsmi_conv3x3_cout1": [_P, _I, _P, _P, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _I, _I, _I, _P],
     "fsmi_dt_layer_floats": [],
     "fsmi_dt_patch_embed": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "fsmi_disparity_transformer": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _F, _P],

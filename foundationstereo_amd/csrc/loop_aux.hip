@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x
 // combine through LDS in wave order (deterministic).
 constexpr int C1O_TR = 2, C1O_TC = 64;
 __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                            float bias, const float* __restrict__ res,
+                                                            const float* __restrict__ bias, const float* __restrict__ res,
                                                             long long res_bstride, float* __restrict__ out,
                                                             long long out_bstride, int Cin, int H, int W, int ntr,
                                                             int ntc, unsigned long long* clk) {
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restr
       float s = part[0][rr * C1O_TC + lane];
 #pragma unroll
       for (int q = 1; q < 4; ++q) s += part[q][rr * C1O_TC + lane];
-      s += bias;
+      if (bias) s += bias[0];
       const long long p = static_cast<long long>(hh) * W + c0;
       if (res) s += res[b * res_bstride + p];
       out[b * out_bstride + p] = s;
@@ -328,7 +328,7 @@ extern "C" int fsmi_resize_bilinear(const float* x, float* out, int B, int C, in
   return finish_launch("fsmi_resize_bilinear");
 }
 
-extern "C" int fsmi_conv3x3_cout1(const float* x, int Cin, const float* w, float bias, const float* res,
+extern "C" int fsmi_conv3x3_cout1(const float* x, int Cin, const float* w, const float* bias, const float* res,
                                   long long res_bstride, float* out, long long out_bstride, int B, int H, int W,
                                   void* stream) {
   FSMI_CHECK_ARG(x && w && out, "fsmi_conv3x3_cout1: null pointer");

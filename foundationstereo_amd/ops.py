@@ -749,10 +749,10 @@ def conv3x3_cout1(x: Tensor, w: Tensor, bias: Tensor = None, res: Tensor = None,
     if res is not None:
         assert res.shape[0] == B and res.shape[1] == 1 and res.shape[2:] == (H, W) and res.stride(2) == W and \
             res.stride(3) == 1, "conv3x3_cout1: res must be (B, 1, H, W) with dense planes"
-    b = float(bias.detach().float().reshape(-1)[0]) if bias is not None else 0.0
+    b = _c(bias.detach().float().reshape(-1)) if bias is not None else None    # device pointer: no sync under capture
     HW = H * W
     _lib.check(_lib.load().fsmi_conv3x3_cout1(
-        _p(x), C, _p(w), b, _p(res) if res is not None else None, res.stride(0) if res is not None else 0,
+        _p(x), C, _p(w), _p(b) if b is not None else None, _p(res) if res is not None else None, res.stride(0) if res is not None else 0,
         out.data_ptr() + 4 * co0 * HW, out.stride(0), B, H, W, _stream(x)), "conv3x3_cout1")
     if _CONV_FLOPS["on"]:
         _CONV_FLOPS["flops"] += 2 * C * 9 * B * HW

@@ -43,9 +43,6 @@ MOTION_ON_MAIN = os.environ.get("FSMI_MOTION_ON_MAIN", "0") != "0"
 
 # SelectiveConvGRU.conv0's context segment convolved once per forward (context_pre); 0: every iteration
 CTX_PRE = os.environ.get("FSMI_CTX_PRE", "1") != "0"
-# run_pipelined: gru04's conv0 / conv1 parts that do not depend on the motion path summed in from partial
-# sums computed off the chain (needs CTX_PRE); 0: the whole convs on the chain
-LOOP_PRE = os.environ.get("FSMI_LOOP_PRE", "1") != "0"
 # DispHead's last conv (128 -> 1) on its own fp32 kernel (ops.conv3x3_cout1); 0: the halo conv tile
 COUT1 = os.environ.get("FSMI_COUT1", "1") != "0"
 # the disparity head writes disp + delta into the next encoder buffer (A/B knob)
@@ -81,8 +78,15 @@ def _packed(*mods, cin_order=None):
         with torch.no_grad():
             ws = [m.weight if m.weight.dim() == 4 else m.weight[:, :, None, None] for m in mods]
             if cin_order is not None:
-                idx = torch.as_tensor(list(cin_order), device=ws[0].device)
-                ws = [w.index_select(1, idx) for w in ws]
+                # runs of consecutive channels as slices: no index tensor to upload (a pack first built
+                # under a stream capture must not copy from the host)
+                runs = []
+                for c in cin_order:
+                    if runs and c == runs[-1][1]:
+                        runs[-1][1] = c + 1
+                    else:
+                        runs.append([c, c + 1])
+                ws = [torch.cat([w[:, a:b] for a, b in runs], 1) for w in ws]
             pk = ops.PackedConv(*ws, mode="halo")
             bias = torch.cat([m.bias.detach().float() for m in mods]).contiguous()
         hit = (key, pk, bias)
@@ -387,21 +391,6 @@ class SelectiveConvGRU(nn.Module):
         pk, b = _packed(self.conv0[0], cin_order=tuple(range(inp.shape[1])))
         return ops.conv2d([inp], pk, bias=b)
 
-    def conv0_partial(self, t, c0, res):
-        """``res + W0[:, c0:c0 + C] * t``: one more loop input's part of conv0 (no bias, no activation)
-        added to a partial sum -- run_pipelined folds gru04's upsampled gru08 state into the context
-        part this way on the pipeline stream, as soon as gru08 has produced it."""
-        pk, _ = _packed(self.conv0[0], cin_order=tuple(range(c0, c0 + t.shape[1])))
-        return ops.conv2d([_f32(t)], pk, res=res)
-
-    def conv1_pre(self, h):
-        """``W1[:, Cx:] * h + b1``: conv1's part of the hidden state h (core/update.py:114-115,
-        ``conv1(cat([conv0(x), h]))``), which needs only h -- run_pipelined computes it beside the
-        disparity head and the motion path, off the chain that ends in conv0."""
-        n = self.conv1[0].in_channels
-        pk, b = _packed(self.conv1[0], cin_order=tuple(range(n - h.shape[1], n)))
-        return ops.conv2d([_f32(h)], pk, bias=b)
-
     def _conv0_rest(self, segs, pre):
         """ReLU(W0[:, segs] * cat(segs) + pre), ``segs`` the (tensor, conv0 input channel offset) pairs
         ``pre`` does not cover (see ``context_pre``).  The first segment's LAST 32 channels go first:
@@ -421,27 +410,20 @@ class SelectiveConvGRU(nn.Module):
         pk, _ = _packed(self.conv0[0], cin_order=tuple(order))
         return ops.conv2d(ss, pk, act="relu_pre", res=pre)
 
-    def forward(self, att, h, *x, pre=None, skip=(0,), pre1=None):
-        """HIP path options (the torch path ignores them; conv0 / conv1 take the whole cats there):
-        ``pre``: conv0's partial sum + bias over the segments ``skip`` of x (``context_pre``, plus
-        ``conv0_partial`` terms); those entries of x are not read and may be given as channel counts.
-        ``pre1``: ``conv1_pre(h)``."""
+    def forward(self, att, h, *x, pre=None):
+        """``pre``: ``context_pre(x[0])`` of this forward's context feature (HIP path; x[0] is then not read;
+        the torch path ignores it, its conv0 takes the whole cat)."""
         if _fast(h):
             h = _f32(h)
             if pre is not None:
-                segs, c = [], 0
-                for i, t in enumerate(x):
-                    if i not in skip:
-                        segs.append((_f32(t), c))
-                    c += t if isinstance(t, int) else t.shape[1]
+                segs, c = [], x[0].shape[1]
+                for t in x[1:]:
+                    segs.append((_f32(t), c))
+                    c += t.shape[1]
                 xc = self._conv0_rest(segs, pre)
             else:
                 xc = _conv(self.conv0[0], _f32s(x), "relu")          # cat(x) as input segments
-            if pre1 is not None:
-                pk, _ = _packed(self.conv1[0], cin_order=tuple(range(self.conv1[0].in_channels - h.shape[1])))
-                hx = ops.conv2d([xc], pk, act="relu_pre", res=pre1)
-            else:
-                hx = _conv(self.conv1[0], [xc, h], "relu")
+            hx = _conv(self.conv1[0], [xc, h], "relu")
             # gates in the conv epilogues: z / r*h from the stacked zr convs, then each convq reads
             # [r*h, x] as two segments and blends straight into the new state
             if not FUSED_GATES:
@@ -591,15 +573,7 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         the freeing stream has joined the reader, so the caching allocator never recycles memory
         a pending kernel still reads.  Returns (net, mask, disp); the mask head runs in the last
         iteration only (test mode discards the others).  ``pre``: ``context_pre(inp)`` (loop-invariant
-        conv0 parts per level) or None.
-
-        With ``pre`` (and LOOP_PRE) gru04's conv0 and conv1 are split by input channels (conv is linear
-        in them, core/update.py:112-115) so that the chain motion(t) -> gru04(t) -> head(t) carries only
-        the parts that depend on motion(t): conv0 over the motion features alone, conv1 over conv0's
-        output alone.  The rest is summed into their epilogues (act 7) from partial sums computed off
-        the chain: q0 = context part + W0[upsampled gru08(t)] on the pipeline stream right after
-        gru08(t) (its resize moves there too), r1 = W1[h] * n0(t-1) + b1 on the branch stream right
-        after gru04(t-1), beside the disparity head and the motion path."""
+        conv0 parts per level) or None."""
         dev = disp.device
         main = torch.cuda.current_stream(dev)
         s_mot, s_gru = _side_stream(dev, 0), _side_stream(dev, 3)
@@ -608,24 +582,11 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
         B, _, H, W = disp.shape
         main_branch = PIPE_BRANCH                        # gru04's small branch on stream 1 (4th stream)
         nc = self.encoder.conv.out_channels
-        loop_pre = LOOP_PRE and p0 is not None
-        if loop_pre:
-            s_br = _side_stream(dev, 1)
-            c_up = inp[0].shape[1] + nc + 1              # gru04.conv0 input: cat(inp0, motion, interp(n1))
-            g4 = self.gru04
-
-            def r1_next(h):                              # conv1's hidden-state part, on the branch stream
-                stream_wait(s_br, main)
-                with torch.cuda.stream(s_br):
-                    return g4.conv1_pre(h)
-            r1 = r1_next(n0)
         stream_wait(s_gru, main)
         _BRANCH[0] = 0                                   # pipeline-stream GRUs: branches in order
         with torch.cuda.stream(s_gru):
             n2 = self.gru16(att[2], n2, inp[2], pool2x(n1), pre=p2)
             n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), interp(n2, n1), pre=p1)
-            if loop_pre:
-                q0 = g4.conv0_partial(interp(n1, n0), c_up, p0)
         _BRANCH[0] = 1
         mask = None
         # the disparity lives in the last channel of the encoder output it feeds: the disparity head
@@ -643,11 +604,9 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 stream_wait(s_mot, main)
                 with torch.cuda.stream(s_mot):
                     self.encoder.motion_into(disp, geo_fn, enc)
-            stream_wait(main, s_gru)                      # gru08(t) (+ q0): enqueued last on s_gru so far
+            stream_wait(main, s_gru)                      # gru08(t): enqueued last on s_gru so far
             if not MOTION_ON_MAIN:
                 stream_wait(main, s_mot)                  # motion(t)
-            if loop_pre:
-                stream_wait(main, s_br)                   # r1(t)
             if t + 1 < iters:
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru16(t+1), beside gru04(t)
@@ -657,13 +616,8 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                     up2 = interp(n2, n1) if EARLY_INTERP else None
                 _BRANCH[0] = 1
             _BRANCH[0] = 1 if main_branch else 0
-            if loop_pre:
-                n0 = g4(att[0], n0, inp[0].shape[1], enc, n1.shape[1], pre=q0, skip=(0, 2), pre1=r1)
-            else:
-                n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0), pre=p0)
+            n0 = self.gru04(att[0], n0, inp[0], enc, interp(n1, n0), pre=p0)
             _BRANCH[0] = 1
-            if loop_pre and t + 1 < iters:
-                r1 = r1_next(n0)
             if t + 1 < iters:
                 stream_wait(s_gru, main)                  # gru04(t)
                 # gru08's branches in order on the pipeline stream: a fork from it would be a side
@@ -671,8 +625,6 @@ class BasicSelectiveMultiUpdateBlock(nn.Module):
                 _BRANCH[0] = 0
                 with torch.cuda.stream(s_gru):           # gru08(t+1), beside the heads + motion(t+1)
                     n1 = self.gru08(att[1], n1, inp[1], pool2x(n0), up2 if EARLY_INTERP else interp(n2, n1), pre=p1)
-                    if loop_pre:
-                        q0 = g4.conv0_partial(interp(n1, n0), c_up, p0)
                 _BRANCH[0] = 1
             if t + 1 == iters:
                 # test mode upsamples only the last iteration's disparity: the reference computes the

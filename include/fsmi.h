@@ -283,10 +283,10 @@ int fsmi_edgenext_mlp(const float* x, const float* res, float* out, const void* 
                       int B, int C, int E, int H, int W, void* stream);
 int fsmi_resize_bilinear(const float* x, float* out, int B, int C, int Hi, int Wi, int Ho, int Wo, void* stream);
 /* fsmi_conv3x3_cout1: Conv2d(Cin, 1, 3, padding=1) + bias (+ res) in fp32 on (B,Cin,H,W) (dense NCHW):
- * out[b*out_bstride + p] = res[b*res_bstride + p] + bias + sum_c,tap w[c*9 + tap] * x[b, c, p + tap];
- * res may be NULL.  DispHead's last layer (core/update.py:28), whose caller adds disp (the loop's
+ * out[b*out_bstride + p] = res[b*res_bstride + p] + bias[0] + sum_c,tap w[c*9 + tap] * x[b, c, p + tap];
+ * bias (device, 1 float) and res may be NULL.  DispHead's last layer (core/update.py:28), whose caller adds disp (the loop's
  * disp + delta, core/foundation_stereo.py:240-241) and writes it into the next motion-feature buffer. */
-int fsmi_conv3x3_cout1(const float* x, int Cin, const float* w, float bias, const float* res, long long res_bstride,
+int fsmi_conv3x3_cout1(const float* x, int Cin, const float* w, const float* bias, const float* res, long long res_bstride,
                        float* out, long long out_bstride, int B, int H, int W, void* stream);
 
 /* fsmi_conv2d_1in: Conv2d(1, Cout, KS, padding=KS//2) (+ ReLU when relu != 0) on (B,1,H,W) ->

@@ -8,8 +8,8 @@ forward and the loop's conv0 convolves only ``rest`` with the halo kernel's act 
   reduce kernels vs fp64 torch (tolerance of the other halo conv tests: 2e-5 abs + 1e-5 rel);
 * SelectiveConvGRU with ``pre`` vs the oracle's restatement (core/update.py:98-119), with a large
   disparity-like last channel in the motion segment (the segment reordering for the block exponent);
-* gru04's run_pipelined split (conv0_partial / conv1_pre) vs the oracle;
-* the product forward with context_pre (FSMI_CTX_PRE) and the loop split (FSMI_LOOP_PRE) on vs off.
+* the product forward with context_pre (FSMI_CTX_PRE) and DispHead's Cout=1 kernel (FSMI_COUT1) on vs
+  off.
 """
 import pytest
 import torch
@@ -95,19 +95,13 @@ def test_selective_gru_with_pre_vs_oracle(ops_mod, HW, disp):
     ref = oracle.stereo_oracle.selective_gru(P, "m", t(att), t(h), t(inp), t(mot), t(up))
     _check(out, ref, "SelectiveConvGRU with context_pre")
     _check(plain, ref, "SelectiveConvGRU")
-    # run_pipelined's split: the upsampled state folded into the context part, conv1's hidden part apart
-    with torch.no_grad():
-        q0 = mod.conv0_partial(g(up), 2 * Ci, pre)
-        r1 = mod.conv1_pre(g(h))
-        split = mod(g(att), g(h), Ci, g(mot), Ci, pre=q0, skip=(0, 2), pre1=r1)
-    _check(split, ref, "SelectiveConvGRU, conv0 / conv1 split by inputs")
 
 
-@pytest.mark.parametrize("knob", ["CTX_PRE", "LOOP_PRE"])
+@pytest.mark.parametrize("knob", ["CTX_PRE", "COUT1"])
 def test_forward_pre_on_off(ops_mod, monkeypatch, knob):
-    """The product forward (pipelined loop) with the conv0 context part hoisted (CTX_PRE) and gru04's
-    conv0 / conv1 split off the chain (LOOP_PRE) vs without: equal to fp32 reordering (and within the
-    oracle's bar in the end-to-end tests)."""
+    """The product forward (pipelined loop) with the conv0 context part hoisted (CTX_PRE) / the fp32
+    Cout=1 head conv (COUT1) vs without: equal to fp32 reordering (and within the oracle's bar in the
+    end-to-end tests)."""
     from foundationstereo_amd import update
     from foundationstereo_amd.foundation_stereo import FoundationStereo
     args = synth.make_args(max_disp=64, corr_levels=2, vit_size="vits")
@@ -125,3 +119,4 @@ def test_forward_pre_on_off(ops_mod, monkeypatch, knob):
             outs[on] = m(g(left), g(right), iters=6, test_mode=True).cpu()
     d = float((outs[True] - outs[False]).abs().max())
     assert d < 1e-4, f"|dd| {knob} on vs off {d:.3g} px"
+

@@ -128,6 +128,11 @@ def no_split(monkeypatch):
     # split-K can put inp[0]'s chunks and the motion chunks in different blocks (each split takes
     # its own first-chunk exponent); one split per conv makes the overflow certain
     monkeypatch.setattr(ops, "_SPLIT_MAXPIX", 10 ** 9)
+    # the trigger is a small FIRST segment of gru04.conv0 (inp[0]); with the context part hoisted
+    # (update.CTX_PRE) inp[0] is convolved alone, uniformly scaled, and cannot overflow -- these tests
+    # exercise the guard / recovery machinery, so they run conv0 whole
+    from foundationstereo_amd import update
+    monkeypatch.setattr(update, "CTX_PRE", False)
 
 
 def test_forward_recovers_from_overflow(lib, no_split):
@@ -204,3 +209,22 @@ def test_captured_forward_poisons_on_overflow(lib, no_split):
     assert bool(torch.isnan(out).all())
     with pytest.raises(ops.RangeError):
         ops.check_range()
+
+
+def test_context_pre_has_no_mixed_scale_chunk(lib, monkeypatch):
+    """The same scaled model with gru04.conv0's context part hoisted (update.CTX_PRE, the default): inp[0]
+    is convolved alone, so no block mixes its 2^-14 chunk with the motion features -- no overflow, no
+    recovery, and the oracle's result."""
+    from foundationstereo_amd import update
+    monkeypatch.setattr(ops, "_SPLIT_MAXPIX", 10 ** 9)
+    monkeypatch.setattr(update, "CTX_PRE", True)
+    args = synth.make_args(max_disp=MD, corr_levels=L, vit_size="vits")
+    m, left, right, ref = _overflowing_model(args)
+    ops.set_range_safe(False)
+    ops.range_overflowed(reset=True)
+    n0 = ops.RANGE_RECOVERIES[0]
+    with torch.no_grad():
+        out = m(left, right, iters=ITERS, test_mode=True)
+    assert ops.RANGE_RECOVERIES[0] == n0 and not ops.range_overflowed(reset=True)
+    d = float((out.cpu() - ref).abs().max())
+    assert d < 1e-3, d
