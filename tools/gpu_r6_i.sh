@@ -1,5 +1,5 @@
 # round-6 GPU step I: hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4) for the replayed
-# 4-stream step: same-box cfg2 A/B 4 / 8 / 16, three alternating rounds
+# 4-stream step: same-box cfg2 A/B 4 / 8 / 16, and the motion path on the main stream, three alternating rounds
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1
@@ -14,5 +14,6 @@ for r in 1 2 3; do
   ab q4_r$r GPU_MAX_HW_QUEUES=4 || exit $?
   ab q8_r$r GPU_MAX_HW_QUEUES=8 || exit $?
   ab q16_r$r GPU_MAX_HW_QUEUES=16 || exit $?
+  ab motion_main_r$r FSMI_MOTION_ON_MAIN=1 || exit $?
 done
 cat $O/ab.txt
