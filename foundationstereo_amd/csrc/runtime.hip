@@ -53,10 +53,12 @@ bool take(int k, hipEvent_t* s, hipEvent_t* e) {
 }  // namespace
 
 // in-kernel clock: a device arena of per-wave (start, end) stamps, bump-allocated per launch and
-// zeroed at enable / reset; per kernel the host keeps (offset, nwaves) of each launch.  4M stamps (32 MB)
-// serve timer modes 1 / 2 (bench.py: only the geometry kernels stamp); timer mode 3 (the timeline
-// build's whole forward) grows it to 64M (512 MB) when no captured graph holds slots in it
-constexpr size_t kClockArenaSmall = size_t(1) << 22;
+// zeroed at enable / reset; per kernel the host keeps (offset, nwaves) of each launch.  16M stamps (128 MB)
+// serve timer modes 1 / 2 (bench.py: only the geometry kernels stamp -- the hierarchical cfg5 step's
+// captured lookups alone take ~6M, reserved for the process, plus as many for the eager pass after it;
+// 4M stamps failed cfg3's and cfg5's lines); timer mode 3 (the timeline build's whole forward) grows it
+// to 64M (512 MB) when no captured graph holds slots in it
+constexpr size_t kClockArenaSmall = size_t(1) << 24;
 constexpr size_t kClockArenaBig = size_t(1) << 26;
 size_t g_clock_cap = 0;                                // stamps allocated
 unsigned long long* g_clock = nullptr;

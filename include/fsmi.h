@@ -414,7 +414,7 @@ int fsmi_timer_query_clock(int kernel, double* total_ms, long long* count);
  * the last replay of each graph.  Kept across fsmi_timer_reset / fsmi_timer_enable (the graphs keep
  * writing their slots) until fsmi_timer_release_captured, which the caller may call only once every
  * graph captured in mode 2 is destroyed (their slots are then handed out again).  Either query fails
- * (FSMI_ERR_ARG) when a launch of the kernel found the clock arena full (4M stamps; 64M in timer mode 3). */
+ * (FSMI_ERR_ARG) when a launch of the kernel found the clock arena full (16M stamps; 64M in timer mode 3). */
 int fsmi_timer_query_clock_captured(int kernel, double* total_ms, long long* count);
 int fsmi_timer_release_captured(void);
 /* The replay's timeline: one text line per launch captured in timer mode 2, in capture order,
