@@ -66,3 +66,35 @@ def test_lookup_clock_in_captured_graph():
         assert n == 1 and 0.0 < ms < 5.0, (ms, n)
     finally:
         ops.timer_enable(False)
+
+
+@pytest.mark.gpu
+def test_clock_arena_holds_a_cfg5_step():
+    """bench.py's timer mode 2 at cfg5 scale: 32 lookups of the 1536x1024 pass (384 x 256 at 1/4, 49k waves
+    each) baked into a graph, then 32 eager ones -- ~6M stamps, beyond the 4M arena that failed the cfg3 /
+    cfg5 bench lines; every launch must be recorded (a full arena makes the query raise)."""
+    from foundationstereo_amd import ops
+    dev = torch.device("cuda:0")
+    B, Cv, D, H, W, L = 1, 28, 48, 256, 384, 4
+    vol = torch.from_numpy(synth.normal(91, (B, Cv, D, H, W))).to(dev)
+    f1, f2 = (torch.from_numpy(synth.normal(s, (B, 32, H, W))).to(dev) for s in (92, 93))
+    corr = ops.allpairs_corr(f1, f2, L)
+    pyr = ops.volume_pyramid(vol, L)
+    disp = torch.from_numpy(synth.uniform(94, (B, 1, H, W), 0.0, D - 1.0)).to(dev)
+    torch.cuda.synchronize()
+    try:
+        ops.timer_enable(True, in_capture=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(32):
+                ops.geo_lookup(pyr, corr, disp, 4)
+        g.replay()
+        for _ in range(32):
+            ops.geo_lookup(pyr, corr, disp, 4)
+        torch.cuda.synchronize()
+        assert ops.timer_query_clock("lookup", captured=True)[1] == 32
+        assert ops.timer_query_clock("lookup")[1] == 32
+        del g
+        ops.timer_release_captured()
+    finally:
+        ops.timer_enable(False)
