@@ -135,6 +135,11 @@ if lk:
          f"post-loop: {(t_last - recs[lk[-1]]['e']) / 1e5:.2f} ms after the last lookup")
     emit("  pre-loop kernel time by family (ms): " + json.dumps(
         {k: round(v / 1e5, 3) for k, v in sorted(fam_pre.items(), key=lambda x: -x[1])[:16]}))
+    # the last iteration (from its lookup) and the post-loop tail (mask head, spx upsampling), every launch
+    t_ll = recs[lk[-1]]["s"]
+    emit("  last iteration + post-loop launches (stream, start / end us from the last lookup, us, tag):")
+    for r in [r for r in recs if r["e"] > t_ll]:
+        emit(f"  {r['stream']:>8} {(r['s'] - t_ll) / 100:8.1f} {(r['e'] - t_ll) / 100:8.1f} {(r['e'] - r['s']) / 100:7.1f}  {r['tag']}")
 if len(lk) > a.iter + 1:
     first, nxt = recs[lk[a.iter]], recs[lk[a.iter + 1]]
     t0, t1 = first["s"], nxt["s"]
